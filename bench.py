@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Word-count throughput on MI355X: input GB/s (whole node) and fraction of the HBM roofline.
+
+A step = one word-count job over device-resident synthetic input (BASELINE.json config 2 per
+GPU: 1 GiB ASCII Zipf, V=1e5, s=1.0, seed 42; rank r gets the r-th GiB of the corpus): reset tables -> map kernel (tokenize +
+aggregate) -> [N > 1: export by owner, RCCL all-to-all-v, import + reduce owned partitions,
+gather to rank 0] -> sort + format the merged "key: count\\n" output in HBM.
+
+  python bench.py --gpus N --steps K --warmup W
+N > 1 is launched by torch.distributed.run (one rank per GPU, backend nccl = RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "mit-6.824-2015_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30)
+    ap.add_argument("--nreduce", type=int, default=64)
+    ap.add_argument("--workload", default="c2_ascii_zipf_1gib")
+    ap.add_argument("--cpu-sample-mib", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per map launch (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, sample_bytes):
+    """The oracle's file-based port of RunSingle (oracle/mr_port.c: Split, DoMap with one JSON
+    write(2) per token, DoReduce, Merge; wc.go's nMap=5, nReduce=3), single thread, on the first
+    `sample_bytes` of the same corpus."""
+    from tests import oracle_bridge as ob
+    from wcg.corpus import Generator
+    data = Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"]).bytes(sample_bytes)
+    d = tempfile.mkdtemp(prefix="wcg-cpu-", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    fname = "cpu-sample.txt"
+    try:
+        with open(os.path.join(d, fname), "wb") as f:
+            f.write(data)
+        t0 = time.perf_counter()
+        rc = ob.run_single_files(d, fname, 5, 3)
+        dt = time.perf_counter() - t0
+        if rc != 0:
+            raise RuntimeError("cpu baseline RunSingle failed")
+        ok = open(os.path.join(d, "mrtmp." + fname), "rb").read() == ob.merged(data)
+    finally:
+        for f in os.listdir(d):
+            os.unlink(os.path.join(d, f))
+        os.rmdir(d)
+    return {"value": round(sample_bytes / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample_bytes >> 20} MiB of the same corpus, RunSingle(nMap=5, nReduce=3) "
+                      f"file-based port incl. split/intermediate/res files on tmpfs ({dt:.1f} s)",
+            "merged_equal_gpu_oracle": ok}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import wcg
+    from wcg.corpus import Generator, CONFIGS, BLOCK
+    from wcg import distributed as wd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("bench.py: N>1 must be launched with torch.distributed.run", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = dict(CONFIGS[args.workload])
+    n = args.bytes_per_gpu
+    # ---- synthetic input for this rank: blocks [rank * n/BLOCK, ...) of the corpus, in HBM
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    gen = Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"])
+    gen.fill_ptr(host.data_ptr(), n, first_block=rank * ((n + BLOCK - 1) // BLOCK))
+    dev = host.to(f"cuda:{local}", non_blocking=False)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream().cuda_stream
+    eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=max(4 * cfg["vocab"], 1 << 18))
+    eng.set_stream(stream)
+    eng.enable_timing(True)
+    teng = wd.TorchEngine(eng, stream)
+    root_eng = None
+    if world > 1 and rank == 0:
+        root_eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=max(4 * cfg["vocab"], 1 << 18))
+        root_eng.set_stream(stream)
+
+    final = {}
+
+    def step():
+        eng.reset()
+        eng.map_device(dev.data_ptr(), n)
+        if world == 1:
+            eng.reduce()
+            final["out"] = eng
+        else:
+            wd.shuffle_reduce(teng, args.nreduce)
+            res = wd.gather_merge(teng, wd.TorchEngine(root_eng, stream) if root_eng else None)
+            final["bytes"] = res
+
+    for _ in range(args.warmup):
+        step()
+    map_ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        map_ms.append(eng.timings()[0][0])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    stats = eng.stats() if world == 1 else None
+
+    # ---- verify the last step's output against the oracle (outside the timed region)
+    verified = None
+    if not args.no_verify:
+        from tests import oracle_bridge as ob
+        if world == 1:
+            got = eng.result()
+            data = host.numpy().tobytes()
+            verified = got == ob.merged(data, 16)
+        else:
+            # every rank sends its input size; root checks token totals via the oracle on its own range
+            verified = None
+
+    if rank == 0:
+        ms_step = dt / args.steps * 1e3
+        total_bytes = n * world
+        gbs = total_bytes / (dt / args.steps) / 1e9
+        avg_map_ms = sum(map_ms) / len(map_ms)
+        achieved = n / (avg_map_ms * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("bytes_per_gpu") == n and tj.get("workload") == args.workload:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        out = {
+            "metric": "word-count input GB/s (whole node) and % of HBM roofline at 1/2/4/8 MI355X",
+            "value": round(gbs, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (csrc/gencorpus.c; kjv12.txt absent)",
+            "config": {"workload": args.workload, "bytes_per_gpu": n, "vocab": cfg["vocab"],
+                       "zipf_s": cfg["zipf_s"], "seed": cfg["seed"], "nreduce": args.nreduce,
+                       "hbm_roofline_frac_whole_step": round(gbs / (HBM_PEAK_GBS * world), 4)},
+            "roofline": {"bound": "hbm", "kernel": "wcg::k_map", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "avg_launch_ms": round(avg_map_ms, 4),
+                         "algorithmic_bytes_per_launch": n},
+        }
+        if stats:
+            out["stats"] = stats
+        out["verified_vs_oracle"] = verified
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample_mib << 20)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,128 @@
+/*
+ * wcg.h - C ABI of the MI355X word-count engine (libwcg.so).
+ *
+ * This is the drop-in boundary for the Lab 1 MapReduce word-count hot path of
+ * wushan270/mit-6.824-2015.  The reference's "plugin API" is a pair of Go function values,
+ *   Map    func(string) *list.List              (/root/reference/src/main/wc.go:17)
+ *   Reduce func(string, *list.List) string      (/root/reference/src/main/wc.go:35)
+ * run by the data plane of package mapreduce
+ *   RunSingle  mapreduce.go:344-356   Split 141-179   DoMap 193-231   ihash 185-189
+ *   DoReduce   mapreduce.go:239-280   Merge 284-321   MapName/ReduceName/MergeName 136,181,233
+ * and by the worker RPC handler Worker.DoJob (worker.go:22-34).
+ *
+ * A GPU backend must implement Map AND Reduce together (the device pre-aggregates
+ * (key, count) pairs, which the per-occurrence CPU Reduce = len(list) could not consume),
+ * so the ABI is phase-shaped - one C call per phase, never one per token:
+ *
+ *   wcg_open     ~ InitMapReduce for a wc job on one GPU            (mapreduce.go:68-82)
+ *   wcg_map*     ~ DoMap(job) + Map over one split's bytes           (mapreduce.go:193-231)
+ *   wcg_reduce   ~ all DoReduce jobs + Merge: sorted "key: count\n"  (mapreduce.go:239-321)
+ *   wcg_partition~ DoReduce(job=r) output bytes mrtmp.<f>-res-<r>    (mapreduce.go:264-279)
+ *   wcg_export / wcg_import ~ the ihash%nReduce shuffle (mapreduce.go:214-230 + 242-263),
+ *                  done as an all-to-all-v of pre-aggregated records between GPUs.
+ *
+ * Conventions:
+ *   - Every entry point returns int status (WCG_OK = 0); the host turns non-zero into a fatal
+ *     error exactly where the reference calls log.Fatal.  wcg_last_error() explains it.
+ *   - Output buffers are library-owned (valid until the next call on the same context).
+ *   - The library never retains caller pointers past a call.
+ *   - Every entry point makes the context's device current (the HIP current device is
+ *     per host thread; Go goroutines migrate between threads).
+ *   - A context is not thread-safe.
+ */
+#ifndef WCG_H
+#define WCG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef WCG_API
+#define WCG_API __attribute__((visibility("default")))
+#endif
+
+typedef struct wcg_ctx wcg_ctx;
+
+enum {
+    WCG_OK = 0,
+    WCG_EINVAL = 1,   /* bad argument                                                */
+    WCG_ENOMEM = 2,   /* device allocation failed                                    */
+    WCG_EHIP = 3,     /* HIP runtime error                                           */
+    WCG_EFULL = 4,    /* aggregation table overflowed (max_keys too small)           */
+    WCG_ESTATE = 5    /* call out of order (e.g. wcg_partition before wcg_reduce)    */
+};
+
+enum {
+    WCG_FMT_MERGED = 0,    /* "key: count\n", all keys, bytewise order  (Merge output)   */
+    WCG_FMT_RES_JSON = 1   /* {"Key":"k","Value":"count"}\n for ihash(k)%R == r          */
+};
+
+/* Open a context on HIP device `device`.
+ *   max_input_bytes: largest single wcg_map() split (sizes the H2D staging buffer; 0 = none,
+ *                    only wcg_map_device() is then allowed)
+ *   max_keys:        capacity in distinct keys of the device aggregation table */
+WCG_API int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx **out);
+WCG_API int wcg_close(wcg_ctx *ctx);
+WCG_API const char *wcg_last_error(const wcg_ctx *ctx);
+
+/* Run all device work of this context on `stream` (a hipStream_t; NULL = the context's own
+ * stream).  Lets a host framework time the phases with its own events. */
+WCG_API int wcg_set_stream(wcg_ctx *ctx, void *stream);
+
+/* Forget all aggregated keys (start a new job). */
+WCG_API int wcg_reset(wcg_ctx *ctx);
+
+/* DoMap + Map (mapreduce.go:193-231, wc.go:17-30) over one split held in host memory:
+ * copy to HBM, tokenize into maximal unicode.IsLetter runs, aggregate (key, count).
+ * Splits must be cut where a token cannot straddle (Split cuts at '\n'). Asynchronous. */
+WCG_API int wcg_map(wcg_ctx *ctx, const uint8_t *host_bytes, uint64_t n);
+
+/* Same, input already resident in device memory (n bytes at dev_bytes). Asynchronous. */
+WCG_API int wcg_map_device(wcg_ctx *ctx, const void *dev_bytes, uint64_t n);
+
+/* DoReduce x nReduce + Merge (mapreduce.go:239-321): sort all keys bytewise on the device and
+ * format the merged file "key: count\n".  Synchronous; returns key count and byte size. */
+WCG_API int wcg_reduce(wcg_ctx *ctx, uint64_t *nkeys, uint64_t *nbytes);
+
+/* Device pointer to / host copy of the formatted output of the last wcg_reduce(). */
+WCG_API int wcg_result_device(wcg_ctx *ctx, const void **dev_ptr, uint64_t *nbytes);
+WCG_API int wcg_result_copy(wcg_ctx *ctx, uint8_t *host_out, uint64_t cap);
+
+/* Bytes of mrtmp.<f>-res-<r> (DoReduce output, mapreduce.go:264-279) for partition r of
+ * nreduce, in sorted key order, copied to host_out (cap bytes).  *nbytes gets the size;
+ * host_out == NULL queries the size only.  Requires a prior wcg_reduce(). */
+WCG_API int wcg_partition(wcg_ctx *ctx, uint32_t nreduce, uint32_t r, uint8_t *host_out, uint64_t cap,
+                  uint64_t *nbytes);
+
+/* ---- multi-GPU shuffle (one process per GPU; the host moves the buffers with RCCL) ----
+ * wcg_export: bucket the local aggregate by owner = (ihash(key) % nreduce) % nranks into a
+ * device buffer of fixed 32-byte records (long keys > 15 bytes are carried in following
+ * 32-byte continuation records).  counts[nranks] receives records per destination, in order.
+ * wcg_import: aggregate records received from peers into this context's table (call after
+ * wcg_reset() on the receiving side, or onto a live table). */
+#define WCG_RECORD_BYTES 32
+WCG_API int wcg_export(wcg_ctx *ctx, uint32_t nreduce, uint32_t nranks, const void **dev_records,
+               uint64_t *counts);
+WCG_API int wcg_import(wcg_ctx *ctx, const void *dev_records, uint64_t nrecords);
+
+/* Per-phase device time of the last pipeline run, in milliseconds, measured with HIP events
+ * on the context's stream: [0] map kernels (sum over wcg_map* calls since wcg_reset),
+ * [1] compaction, [2] sort, [3] format.  Also the number of map kernel launches. */
+WCG_API int wcg_timings(wcg_ctx *ctx, double *ms4, uint64_t *map_launches);
+/* Enable/disable the event timing above (off by default: it adds event records). */
+WCG_API int wcg_enable_timing(wcg_ctx *ctx, int on);
+
+/* Diagnostics: tokens seen, distinct keys, tokens resolved in LDS vs global table, long keys. */
+WCG_API int wcg_stats(wcg_ctx *ctx, uint64_t *stats8);
+
+/* FNV-1a 32 (= ihash, mapreduce.go:185-189), host side, for partition arithmetic. */
+WCG_API uint32_t wcg_ihash(const uint8_t *key, uint64_t len);
+
+WCG_API const char *wcg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WCG_H */

@@ -1,0 +1,467 @@
+// wcg_api.hip - C ABI of libwcg.so (declared in include/wcg.h).
+//
+// One context = one GPU's share of a word-count job.  Device memory is allocated once at
+// wcg_open and sized for 288 GB HBM parts: the aggregation tables, the record buffers for
+// the sort and the formatted output all stay resident, so a job is a fixed sequence of
+// launches on one stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/wcg.h"
+#include "wcg_common.h"
+#include "wcg_map.h"
+#include "wcg_reduce.h"
+
+using namespace wcg;
+
+struct wcg_ctx {
+    int device = 0;
+    int ncu = 256;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    u64 max_input = 0, max_keys = 0;
+    uint8_t* d_in = nullptr;
+    GEntry* gtab = nullptr; u64 gslots = 0;
+    GEntry* ltab = nullptr; u64 lslots = 0;
+    uint8_t* arena = nullptr; u64 arena_cap = 0;
+    DevState* st = nullptr;
+    DevState* h_st = nullptr;                 // pinned mirror
+    Rec* recA = nullptr; Rec* recB = nullptr; u64 rec_cap = 0;
+    Rec* sorted = nullptr;
+    u32* bh = nullptr; u64 bh_cap = 0;
+    u64* lens = nullptr;
+    u64* d_scalar = nullptr;                  // scan totals
+    uint8_t* d_out = nullptr; u64 out_cap = 0; u64 out_len = 0;
+    uint8_t* d_part = nullptr; u64 part_cap = 0;
+    u64 nrec = 0;
+    bool compacted = false, reduced = false;
+    // export
+    u32* owner = nullptr;
+    u64* d_per_rank = nullptr;                // [2 * 1024]: counts, cursors
+    Rec* exp_buf = nullptr; u64 exp_cap = 0;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> map_ev;
+    hipEvent_t phase_ev[6] = {};
+    bool phase_rec = false;
+    u64 map_launches = 0;
+    std::string err;
+};
+
+namespace {
+
+#define HIPCHK(ctx, call)                                                                   \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                 \
+            return WCG_EHIP;                                                                \
+        }                                                                                   \
+    } while (0)
+
+u64 next_pow2(u64 x) {
+    u64 p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+int set_dev(wcg_ctx* c) {
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) { c->err = std::string("hipSetDevice: ") + hipGetErrorString(e); return WCG_EHIP; }
+    return WCG_OK;
+}
+
+int grid_for(u64 n, int nt, int cap) {
+    u64 g = (n + nt - 1) / nt;
+    if (g < 1) g = 1;
+    if (g > (u64)cap) g = cap;
+    return (int)g;
+}
+
+hipEvent_t take_event(wcg_ctx* c) {
+    if (c->ev_used == c->ev_pool.size()) {
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[c->ev_used++];
+}
+
+int check_status(wcg_ctx* c) {
+    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, offsetof(DevState, hist), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_st->overflow || c->h_st->spin_fail) {
+        char buf[256];
+        snprintf(buf, sizeof buf,
+                 "aggregation table full (overflow=%u spin=%u): raise max_keys (%llu) / arena (%llu bytes)",
+                 c->h_st->overflow, c->h_st->spin_fail, (unsigned long long)c->max_keys,
+                 (unsigned long long)c->arena_cap);
+        c->err = buf;
+        return WCG_EFULL;
+    }
+    return WCG_OK;
+}
+
+int ensure(wcg_ctx* c, uint8_t** p, u64* cap, u64 need) {
+    if (need <= *cap) return WCG_OK;
+    u64 nc = std::max<u64>(need + need / 4, 1 << 20);
+    if (*p) HIPCHK(c, hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(c, hipMalloc(p, nc));
+    *cap = nc;
+    return WCG_OK;
+}
+
+int compact(wcg_ctx* c) {
+    if (c->compacted) return WCG_OK;
+    HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, sizeof(u64), c->stream));
+    if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
+    u64 total = c->gslots + c->lslots;
+    k_compact<<<grid_for(total, 256, c->ncu * 16), 256, 0, c->stream>>>(c->gtab, c->gslots, c->ltab, c->lslots,
+                                                                       c->arena, c->recA, c->st);
+    HIPCHK(c, hipGetLastError());
+    if (c->timing) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
+    int rc = check_status(c);
+    if (rc) return rc;
+    c->nrec = c->h_st->nrec;
+    c->compacted = true;
+    return WCG_OK;
+}
+
+// LSD radix sort of recA[0:nrec) by the 128-bit prefix; result pointer in c->sorted
+int sort_records(wcg_ctx* c) {
+    u64 n = c->nrec;
+    c->sorted = c->recA;
+    if (n <= 1) return WCG_OK;
+    HIPCHK(c, hipMemsetAsync(c->st->hist, 0, sizeof(c->st->hist), c->stream));
+    k_hist16<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(c->recA, n, c->st);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->h_st->hist, c->st->hist, sizeof(c->st->hist), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    u32 nblocks = (u32)((n + RS_TILE - 1) / RS_TILE);
+    Rec* src = c->recA;
+    Rec* dst = c->recB;
+    for (int d = 0; d < 16; d++) {
+        bool trivial = false;
+        for (int x = 0; x < 256; x++)
+            if (c->h_st->hist[d][x] == n) { trivial = true; break; }
+        if (trivial) continue;
+        k_digit_hist<<<nblocks, RS_NT, 0, c->stream>>>(src, n, d, c->bh, nblocks);
+        k_scan_u32<<<1, 1024, 0, c->stream>>>(c->bh, (u64)nblocks * 256, nullptr);
+        k_scatter<<<nblocks, RS_NT, 0, c->stream>>>(src, dst, n, d, c->bh, nblocks);
+        HIPCHK(c, hipGetLastError());
+        std::swap(src, dst);
+    }
+    c->sorted = src;
+    // long keys sharing a 16-byte prefix
+    HIPCHK(c, hipMemsetAsync(&c->st->tie_flag, 0, sizeof(u32), c->stream));
+    k_tie_detect<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(c->sorted, n, c->st);
+    HIPCHK(c, hipMemcpyAsync(&c->h_st->tie_flag, &c->st->tie_flag, sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_st->tie_flag) {
+        k_tie_fix<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(c->sorted, n, c->arena);
+        HIPCHK(c, hipGetLastError());
+    }
+    return WCG_OK;
+}
+
+// format sorted records; returns device buffer + size
+int format(wcg_ctx* c, int fmt, u32 nreduce, u32 part, uint8_t** dbuf, u64* cap, u64* nbytes) {
+    u64 n = c->nrec;
+    if (n == 0) { *nbytes = 0; return WCG_OK; }
+    int g = grid_for(n, 256, c->ncu * 8);
+    k_linelen<<<g, 256, 0, c->stream>>>(c->sorted, n, fmt, nreduce, part, c->arena, c->lens);
+    k_scan_u64<<<1, 1024, 0, c->stream>>>(c->lens, n, c->d_scalar);
+    HIPCHK(c, hipGetLastError());
+    u64 total = 0;
+    HIPCHK(c, hipMemcpyAsync(&total, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int rc = ensure(c, dbuf, cap, total + 16);
+    if (rc) return rc;
+    k_write<<<g, 256, 0, c->stream>>>(c->sorted, n, fmt, nreduce, part, c->arena, c->lens, *dbuf);
+    HIPCHK(c, hipGetLastError());
+    *nbytes = total;
+    return WCG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* wcg_version(void) { return "wcg 0.1 gfx950 (unicode " WCG_UNICODE_VERSION ")"; }
+
+const char* wcg_last_error(const wcg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+uint32_t wcg_ihash(const uint8_t* key, uint64_t len) {
+    uint32_t h = 0x811C9DC5u;
+    for (uint64_t i = 0; i < len; i++) { h ^= key[i]; h *= 0x01000193u; }
+    return h;
+}
+
+int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx** out) {
+    if (!out) return WCG_EINVAL;
+    *out = nullptr;
+    wcg_ctx* c = new wcg_ctx();
+    c->device = device;
+    c->max_input = max_input_bytes;
+    c->max_keys = std::max<u64>(max_keys, 1024);
+    int rc = set_dev(c);
+    if (rc) { *out = c; return rc; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->ncu = prop.multiProcessorCount;
+    *out = c;
+    HIPCHK(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    c->stream = c->own_stream;
+    c->gslots = next_pow2(2 * c->max_keys);
+    c->lslots = std::max<u64>(next_pow2(c->gslots / 4), 4096);
+    c->arena_cap = std::max<u64>(64ull << 20, c->lslots * 48);
+    c->rec_cap = c->gslots / 2 + c->lslots / 2 + 16;
+    if (c->max_input) HIPCHK(c, hipMalloc(&c->d_in, c->max_input + 64));
+    HIPCHK(c, hipMalloc(&c->gtab, c->gslots * sizeof(GEntry)));
+    HIPCHK(c, hipMalloc(&c->ltab, c->lslots * sizeof(GEntry)));
+    HIPCHK(c, hipMalloc(&c->arena, c->arena_cap + 64));
+    HIPCHK(c, hipMalloc(&c->st, sizeof(DevState)));
+    HIPCHK(c, hipHostMalloc(&c->h_st, sizeof(DevState), hipHostMallocDefault));
+    // records: compaction output is bounded by the number of occupied slots
+    u64 recs = c->gslots + c->lslots;
+    c->rec_cap = recs;
+    HIPCHK(c, hipMalloc(&c->recA, recs * sizeof(Rec)));
+    HIPCHK(c, hipMalloc(&c->recB, recs * sizeof(Rec)));
+    c->bh_cap = ((recs + RS_TILE - 1) / RS_TILE) * 256 + 256;
+    HIPCHK(c, hipMalloc(&c->bh, c->bh_cap * sizeof(u32)));
+    HIPCHK(c, hipMalloc(&c->lens, recs * sizeof(u64)));
+    HIPCHK(c, hipMalloc(&c->d_scalar, 64));
+    HIPCHK(c, hipMalloc(&c->owner, recs * sizeof(u32)));
+    HIPCHK(c, hipMalloc(&c->d_per_rank, 2 * 1024 * sizeof(u64)));
+    return wcg_reset(c);
+}
+
+int wcg_close(wcg_ctx* c) {
+    if (!c) return WCG_EINVAL;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    void* bufs[] = {c->d_in, c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->bh, c->lens,
+                    c->d_scalar, c->d_out, c->d_part, c->owner, c->d_per_rank, c->exp_buf};
+    for (void* b : bufs) if (b) (void)hipFree(b);
+    if (c->h_st) (void)hipHostFree(c->h_st);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return WCG_OK;
+}
+
+int wcg_set_stream(wcg_ctx* c, void* stream) {
+    if (!c) return WCG_EINVAL;
+    c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    return WCG_OK;
+}
+
+int wcg_enable_timing(wcg_ctx* c, int on) {
+    if (!c) return WCG_EINVAL;
+    c->timing = on != 0;
+    return WCG_OK;
+}
+
+int wcg_reset(wcg_ctx* c) {
+    if (!c) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(c->gtab, 0, c->gslots * sizeof(GEntry), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->ltab, 0, c->lslots * sizeof(GEntry), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->st, 0, offsetof(DevState, hist), c->stream));
+    c->compacted = c->reduced = false;
+    c->nrec = 0;
+    c->out_len = 0;
+    c->map_ev.clear();
+    c->ev_used = 0;
+    c->phase_rec = false;
+    c->map_launches = 0;
+    return WCG_OK;
+}
+
+int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
+    if (!c) return WCG_EINVAL;
+    if (n == 0) return WCG_OK;
+    if (!dev_bytes || ((uintptr_t)dev_bytes & 15)) { c->err = "wcg_map_device: input must be 16-byte aligned"; return WCG_EINVAL; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    MapArgs a;
+    a.in = (const uint8_t*)dev_bytes;
+    a.n = n;
+    a.ntiles = (n + MAP_TILE - 1) / MAP_TILE;
+    u64 grid = std::min<u64>((u64)c->ncu, a.ntiles);
+    a.tiles_per_wg = (a.ntiles + grid - 1) / grid;
+    grid = (a.ntiles + a.tiles_per_wg - 1) / a.tiles_per_wg;
+    a.gtab = c->gtab; a.gmask = c->gslots - 1;
+    a.ltab = c->ltab; a.lmask = c->lslots - 1;
+    a.arena = c->arena; a.arena_cap = c->arena_cap;
+    a.st = c->st;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing) { e0 = take_event(c); HIPCHK(c, hipEventRecord(e0, c->stream)); }
+    k_map<<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a);
+    HIPCHK(c, hipGetLastError());
+    if (c->timing) { e1 = take_event(c); HIPCHK(c, hipEventRecord(e1, c->stream)); c->map_ev.push_back({e0, e1}); }
+    c->map_launches++;
+    c->compacted = c->reduced = false;
+    return WCG_OK;
+}
+
+int wcg_map(wcg_ctx* c, const uint8_t* host_bytes, uint64_t n) {
+    if (!c) return WCG_EINVAL;
+    if (n == 0) return WCG_OK;
+    if (!c->d_in || n > c->max_input) { c->err = "wcg_map: split larger than max_input_bytes"; return WCG_EINVAL; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_in, host_bytes, n, hipMemcpyHostToDevice, c->stream));
+    rc = wcg_map_device(c, c->d_in, n);
+    if (rc) return rc;
+    // the staging buffer is reused by the next call: finish this one first
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return WCG_OK;
+}
+
+int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
+    if (!c) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    if ((rc = compact(c))) return rc;
+    if (c->timing) { c->phase_ev[2] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream)); }
+    if ((rc = sort_records(c))) return rc;
+    if (c->timing) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }
+    if ((rc = format(c, FMT_MERGED, 1, 0, &c->d_out, &c->out_cap, &c->out_len))) return rc;
+    if (c->timing) {
+        c->phase_ev[4] = take_event(c);
+        HIPCHK(c, hipEventRecord(c->phase_ev[4], c->stream));
+        c->phase_rec = true;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->reduced = true;
+    if (nkeys) *nkeys = c->nrec;
+    if (nbytes) *nbytes = c->out_len;
+    return WCG_OK;
+}
+
+int wcg_result_device(wcg_ctx* c, const void** dev_ptr, uint64_t* nbytes) {
+    if (!c) return WCG_EINVAL;
+    if (!c->reduced) { c->err = "wcg_result_device before wcg_reduce"; return WCG_ESTATE; }
+    if (dev_ptr) *dev_ptr = c->d_out;
+    if (nbytes) *nbytes = c->out_len;
+    return WCG_OK;
+}
+
+int wcg_result_copy(wcg_ctx* c, uint8_t* host_out, uint64_t cap) {
+    if (!c) return WCG_EINVAL;
+    if (!c->reduced) { c->err = "wcg_result_copy before wcg_reduce"; return WCG_ESTATE; }
+    if (cap < c->out_len) { c->err = "wcg_result_copy: buffer too small"; return WCG_EINVAL; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    if (c->out_len) {
+        HIPCHK(c, hipMemcpyAsync(host_out, c->d_out, c->out_len, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return WCG_OK;
+}
+
+int wcg_partition(wcg_ctx* c, uint32_t nreduce, uint32_t r, uint8_t* host_out, uint64_t cap, uint64_t* nbytes) {
+    if (!c) return WCG_EINVAL;
+    if (!c->reduced) { c->err = "wcg_partition before wcg_reduce"; return WCG_ESTATE; }
+    if (nreduce == 0 || r >= nreduce) { c->err = "wcg_partition: bad partition"; return WCG_EINVAL; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    u64 len = 0;
+    if ((rc = format(c, FMT_JSON, nreduce, r, &c->d_part, &c->part_cap, &len))) return rc;
+    if (nbytes) *nbytes = len;
+    if (host_out) {
+        if (cap < len) { c->err = "wcg_partition: buffer too small"; return WCG_EINVAL; }
+        if (len) HIPCHK(c, hipMemcpyAsync(host_out, c->d_part, len, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return WCG_OK;
+}
+
+int wcg_export(wcg_ctx* c, uint32_t nreduce, uint32_t nranks, const void** dev_records, uint64_t* counts) {
+    if (!c || !counts || nreduce == 0 || nranks == 0 || nranks > 1024) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    if ((rc = compact(c))) return rc;
+    u64 n = c->nrec;
+    HIPCHK(c, hipMemsetAsync(c->d_per_rank, 0, 2 * 1024 * sizeof(u64), c->stream));
+    if (n) {
+        k_export_count<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recA, n, nreduce, nranks, c->arena,
+                                                                             c->owner, c->d_per_rank);
+        HIPCHK(c, hipGetLastError());
+    }
+    std::vector<u64> per(nranks), cur(nranks);
+    HIPCHK(c, hipMemcpyAsync(per.data(), c->d_per_rank, nranks * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    u64 tot = 0;
+    for (u32 i = 0; i < nranks; i++) { cur[i] = tot; tot += per[i]; counts[i] = per[i]; }
+    rc = ensure(c, reinterpret_cast<uint8_t**>(&c->exp_buf), &c->exp_cap, (tot + 1) * sizeof(Rec));
+    if (rc) return rc;
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(c->d_per_rank + 1024, cur.data(), nranks * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+        k_export_write<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recA, n, c->owner, c->d_per_rank + 1024,
+                                                                             c->arena, c->exp_buf);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (dev_records) *dev_records = c->exp_buf;
+    return WCG_OK;
+}
+
+int wcg_import(wcg_ctx* c, const void* dev_records, uint64_t nrecords) {
+    if (!c) return WCG_EINVAL;
+    if (nrecords == 0) return WCG_OK;
+    if (!dev_records) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    k_import<<<grid_for(nrecords, 256, c->ncu * 8), 256, 0, c->stream>>>((const Rec*)dev_records, nrecords, c->gtab,
+                                                                          c->gslots - 1, c->ltab, c->lslots - 1,
+                                                                          c->arena, c->arena_cap, c->st);
+    HIPCHK(c, hipGetLastError());
+    c->compacted = c->reduced = false;
+    return check_status(c);
+}
+
+int wcg_timings(wcg_ctx* c, double* ms4, uint64_t* map_launches) {
+    if (!c || !ms4) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 4; i++) ms4[i] = 0;
+    for (auto& p : c->map_ev) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, p.first, p.second));
+        ms4[0] += ms;
+    }
+    if (c->phase_rec) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->phase_ev[0], c->phase_ev[1])); ms4[1] = ms;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->phase_ev[2], c->phase_ev[3])); ms4[2] = ms;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->phase_ev[3], c->phase_ev[4])); ms4[3] = ms;
+    }
+    if (map_launches) *map_launches = c->map_launches;
+    return WCG_OK;
+}
+
+int wcg_stats(wcg_ctx* c, uint64_t* s8) {
+    if (!c || !s8) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, offsetof(DevState, hist), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    s8[0] = c->h_st->tokens; s8[1] = c->nrec; s8[2] = c->h_st->lds_hits; s8[3] = c->h_st->global_ops;
+    s8[4] = c->h_st->long_tokens; s8[5] = c->h_st->arena_top; s8[6] = c->h_st->overflow; s8[7] = c->h_st->spin_fail;
+    return WCG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,188 @@
+// wcg_common.h - device-side building blocks of the MI355X word-count engine (gfx950).
+//
+// Semantics restated (reference paths relative to /root/reference):
+//   token   = maximal run of runes with unicode.IsLetter (src/main/wc.go:18-21,
+//             strings.FieldsFunc); runes decoded with Go's utf8 rules, an invalid byte is
+//             U+FFFD of width 1 (a separator).
+//   ihash   = FNV-1a 32 (src/mapreduce/mapreduce.go:185-189).
+//
+// Byte-level facts the kernels rely on (proved in DESIGN.md section 3):
+//   F1  every byte that is not a UTF-8 continuation byte (80..BF) starts a rune in Go's
+//       decoding, so a byte's letter-ness depends only on bytes [p-3, p+3];
+//   F2  a 16-byte chunk whose bytes are all < 0x80 is ASCII regardless of its neighbours;
+//   F3  tokens are the maximal runs of "letter bytes"; a token start is a letter byte whose
+//       predecessor is not a letter byte, and it is always a rune start;
+//   F4  letters never contain the byte 0x00, so a key of <= 15 bytes zero-padded to 16 bytes
+//       (+ its length in byte 15) is an exact, fixed-width identity, and big-endian
+//       comparison of the zero-padded bytes is Go's bytewise string order (sort.Strings).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define WCG_LT_QUAL __constant__
+#include "letter_table.h"
+
+namespace wcg {
+
+typedef unsigned long long u64;
+typedef unsigned int u32;
+
+// ---- global aggregation table entry (HBM).  inline keys: k0 = bytes 0-7 (LE),
+// k1 = bytes 8-14 | len << 56 (len 1..15, so k1 != 0 once published); cnt = occurrences.
+// long-key table: k0 = 64-bit hash tag (|1), k1 = arena offset + 1 (publish word),
+// aux = key length.
+struct __align__(32) GEntry { u64 k0, k1, cnt, aux; };
+
+// ---- sorted record (after compaction): the 128-bit big-endian prefix is the sort key.
+// inline: ref = len (1..15); long: ref = LONG_FLAG | len << 40 | arena offset.
+struct __align__(32) Rec { u64 hi, lo, cnt, ref; };
+constexpr u64 LONG_FLAG = 1ull << 63;
+constexpr u64 LONG_OFF_MASK = (1ull << 40) - 1;
+constexpr u64 LONG_LEN_MAX = (1ull << 23) - 1;
+
+// ---- device-side counters/status (one per context)
+struct DevState {
+    u64 tokens;          // tokens seen by map kernels
+    u64 lds_hits;        // tokens aggregated in LDS
+    u64 global_ops;      // global-table insertions (misses + flushes)
+    u64 long_tokens;     // tokens longer than 15 bytes
+    u64 arena_top;       // bytes used in the long-key arena
+    u64 nrec;            // records produced by compaction
+    u32 overflow;        // table / arena full -> WCG_EFULL
+    u32 spin_fail;       // bounded spin gave up -> WCG_EFULL (never expected)
+    u32 tie_flag;        // two long keys share a 16-byte prefix
+    u32 pad;
+    u64 hist[16][256];   // global digit histograms for the sort
+};
+
+// ------------------------------------------------------------------ letters
+__device__ __forceinline__ bool lt_is_letter(u32 cp) {
+    if (cp < 0x80) return ((cp | 0x20) - 'a') < 26u;
+    if (cp >= 0x110000) return false;
+    u32 blk = WCG_LT_STAGE1[cp >> 8];
+    return (WCG_LT_STAGE2[blk][(cp >> 5) & 7] >> (cp & 31)) & 1u;
+}
+
+// Go utf8.DecodeRune at p of a byte source `at(i)` returning 0 beyond the end.
+// Returns width (0 = invalid -> treat as RuneError width 1) and the code point.
+template <typename At>
+__device__ __forceinline__ int go_decode(At at, long p, u32* cp_out) {
+    u32 b0 = at(p);
+    if (b0 < 0x80) { *cp_out = b0; return 1; }
+    int w; u32 lo = 0x80, hi = 0xBF;
+    if (b0 >= 0xC2 && b0 <= 0xDF) w = 2;
+    else if (b0 >= 0xE0 && b0 <= 0xEF) { w = 3; if (b0 == 0xE0) lo = 0xA0; else if (b0 == 0xED) hi = 0x9F; }
+    else if (b0 >= 0xF0 && b0 <= 0xF4) { w = 4; if (b0 == 0xF0) lo = 0x90; else if (b0 == 0xF4) hi = 0x8F; }
+    else return 0;
+    u32 b1 = at(p + 1);
+    if (b1 < lo || b1 > hi) return 0;
+    if (w == 2) { *cp_out = ((b0 & 0x1F) << 6) | (b1 & 0x3F); return 2; }
+    u32 b2 = at(p + 2);
+    if ((b2 & 0xC0) != 0x80) return 0;
+    if (w == 3) { *cp_out = ((b0 & 0x0F) << 12) | ((b1 & 0x3F) << 6) | (b2 & 0x3F); return 3; }
+    u32 b3 = at(p + 3);
+    if ((b3 & 0xC0) != 0x80) return 0;
+    *cp_out = ((b0 & 0x07) << 18) | ((b1 & 0x3F) << 12) | ((b2 & 0x3F) << 6) | (b3 & 0x3F);
+    return 4;
+}
+
+// Is byte p part of a letter rune?  (fact F1: look back at most 3 bytes for the lead)
+template <typename At>
+__device__ __forceinline__ bool letter_byte(At at, long p) {
+    u32 b = at(p);
+    if (b < 0x80) return ((b | 0x20) - 'a') < 26u;
+    u32 cp;
+    if ((b & 0xC0) == 0x80) {
+        for (int k = 1; k <= 3; k++) {
+            u32 q = at(p - k);
+            if ((q & 0xC0) == 0x80) continue;          // another continuation byte
+            int w = go_decode(at, p - k, &cp);
+            return w > k && lt_is_letter(cp);         // covered by a valid rune starting at p-k
+        }
+        return false;                                 // 4+ continuation bytes: invalid
+    }
+    int w = go_decode(at, p, &cp);
+    return w > 0 && lt_is_letter(cp);
+}
+
+// 16 ASCII bytes (4 little-endian dwords) -> 16-bit letter mask (SWAR, bytes < 0x80 only)
+__device__ __forceinline__ u32 ascii_mask4(u32 x) {
+    u32 t = x | 0x20202020u;
+    u32 a = t + 0x1F1F1F1Fu;            // >= 'a'  (no carries: t <= 0x7F per byte)
+    u32 b = t + 0x05050505u;            // >= '{'
+    u32 hi = a & ~b & 0x80808080u;
+    return (((hi >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+__device__ __forceinline__ u32 ascii_mask16(uint4 v) {
+    return ascii_mask4(v.x) | (ascii_mask4(v.y) << 4) | (ascii_mask4(v.z) << 8) | (ascii_mask4(v.w) << 12);
+}
+__device__ __forceinline__ bool all_ascii(uint4 v) { return ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0; }
+
+// ------------------------------------------------------------------ hashing
+__device__ __host__ __forceinline__ u64 mix64(u64 x) {
+    x ^= x >> 32; x *= 0xD6E8FEB86659FD93ull; x ^= x >> 32; x *= 0xD6E8FEB86659FD93ull; x ^= x >> 32;
+    return x;
+}
+__device__ __forceinline__ u64 key_hash(u64 k0, u64 k1) {
+    return mix64(k0 * 0x9E3779B97F4A7C15ull + (k1 ^ (k1 >> 29)) * 0xC2B2AE3D27D4EB4Full);
+}
+__device__ __forceinline__ u32 fnv1a_step(u32 h, u32 byte) { return (h ^ byte) * 0x01000193u; }
+
+__device__ __forceinline__ u64 bswap64(u64 x) { return __builtin_bswap64(x); }
+
+// mask keeping the low `nbytes` bytes (0..8)
+__device__ __forceinline__ u64 low_bytes_mask(int nbytes) {
+    return nbytes >= 8 ? ~0ull : ((1ull << (8 * nbytes)) - 1);
+}
+
+// ------------------------------------------------------------------ atomics helpers
+__device__ __forceinline__ u64 ld_agent(const u64* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(u64* p, u64 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool cas_agent(u64* p, u64* expected, u64 desired) {
+    return __hip_atomic_compare_exchange_strong(p, expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void add_agent(u64* p, u64 v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int SPIN_LIMIT = 1 << 20;
+
+// Insert/accumulate an inline key into the global table (open addressing, linear probing).
+// Claim protocol: CAS k0 0->key, then publish k1 (never 0 for a valid key).  A reader that
+// sees k0 == key but k1 == 0 re-reads in a later iteration (the claimer publishes in the same
+// iteration of its own loop, so no lane waits on a lane parked behind it).
+__device__ __forceinline__ void ginsert(GEntry* tab, u64 mask, u64 k0, u64 k1, u64 h, u64 cnt, DevState* st) {
+    u64 s = h & mask;
+    u64 probes = 0;
+    int spins = 0;
+    while (true) {
+        GEntry* e = &tab[s];
+        u64 c0 = ld_agent(&e->k0);
+        if (c0 == 0) {
+            u64 exp = 0;
+            if (cas_agent(&e->k0, &exp, k0)) {
+                st_agent(&e->k1, k1);
+                add_agent(&e->cnt, cnt);
+                return;
+            }
+            c0 = exp;
+        }
+        if (c0 == k0) {
+            u64 c1 = ld_agent(&e->k1);
+            if (c1 == k1) { add_agent(&e->cnt, cnt); return; }
+            if (c1 == 0) {                                   // claimed, not yet published
+                if (++spins > SPIN_LIMIT) { atomicAdd(&st->spin_fail, 1u); return; }
+                continue;
+            }
+        }
+        s = (s + 1) & mask;
+        if (++probes > mask) { atomicAdd(&st->overflow, 1u); return; }
+    }
+}
+
+}  // namespace wcg

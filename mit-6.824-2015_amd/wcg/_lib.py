@@ -1,0 +1,184 @@
+"""ctypes binding of libwcg.so (C ABI declared in include/wcg.h).
+
+The product path has no CPU fallback: if libwcg.so is missing or no GPU is visible, opening an
+engine raises.  Build the library with `python -c "import __graft_entry__ as g; g.build()"`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Tuple
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwcg.so")
+
+WCG_OK, WCG_EINVAL, WCG_ENOMEM, WCG_EHIP, WCG_EFULL, WCG_ESTATE = range(6)
+RECORD_BYTES = 32
+
+_lib: Optional[ctypes.CDLL] = None
+
+# every symbol include/wcg.h declares (tests check the library exports them all)
+EXPORTED = [
+    "wcg_open", "wcg_close", "wcg_last_error", "wcg_set_stream", "wcg_reset", "wcg_map",
+    "wcg_map_device", "wcg_reduce", "wcg_result_device", "wcg_result_copy", "wcg_partition",
+    "wcg_export", "wcg_import", "wcg_timings", "wcg_enable_timing", "wcg_stats", "wcg_ihash",
+    "wcg_version",
+]
+
+
+class WcgError(RuntimeError):
+    """Non-zero status from libwcg (the reference would log.Fatal at this point)."""
+
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"wcg status {status}: {msg}")
+        self.status = status
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run __graft_entry__.build() (hipcc gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, U64, U32, I = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    PU64 = ctypes.POINTER(ctypes.c_uint64)
+    sig = {
+        "wcg_open": (I, [I, U64, U64, ctypes.POINTER(P)]),
+        "wcg_close": (I, [P]),
+        "wcg_last_error": (ctypes.c_char_p, [P]),
+        "wcg_set_stream": (I, [P, P]),
+        "wcg_reset": (I, [P]),
+        "wcg_map": (I, [P, ctypes.c_char_p, U64]),
+        "wcg_map_device": (I, [P, P, U64]),
+        "wcg_reduce": (I, [P, PU64, PU64]),
+        "wcg_result_device": (I, [P, ctypes.POINTER(P), PU64]),
+        "wcg_result_copy": (I, [P, P, U64]),
+        "wcg_partition": (I, [P, U32, U32, P, U64, PU64]),
+        "wcg_export": (I, [P, U32, U32, ctypes.POINTER(P), PU64]),
+        "wcg_import": (I, [P, P, U64]),
+        "wcg_timings": (I, [P, ctypes.POINTER(ctypes.c_double), PU64]),
+        "wcg_enable_timing": (I, [P, I]),
+        "wcg_stats": (I, [P, PU64]),
+        "wcg_ihash": (U32, [ctypes.c_char_p, U64]),
+        "wcg_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def ihash(key: bytes) -> int:
+    """FNV-1a 32 (mapreduce.go:185-189) via the library's host helper."""
+    return load().wcg_ihash(key, len(key))
+
+
+class Engine:
+    """One GPU's word-count context (wraps wcg_ctx).
+
+    Phase methods mirror the reference data plane: map_* = DoMap+Map over a split,
+    reduce() = DoReduce x R + Merge, partition() = one DoReduce output file."""
+
+    def __init__(self, device: int = 0, max_input_bytes: int = 0, max_keys: int = 1 << 20):
+        self._lib = load()
+        self._ctx = ctypes.c_void_p()
+        rc = self._lib.wcg_open(device, max_input_bytes, max_keys, ctypes.byref(self._ctx))
+        if rc != WCG_OK:
+            msg = self._lib.wcg_last_error(self._ctx).decode() if self._ctx else "open failed"
+            if self._ctx:
+                self._lib.wcg_close(self._ctx)
+                self._ctx = ctypes.c_void_p()
+            raise WcgError(rc, msg)
+        self.device = device
+
+    # -- plumbing
+    def _chk(self, rc: int) -> None:
+        if rc != WCG_OK:
+            raise WcgError(rc, self._lib.wcg_last_error(self._ctx).decode())
+
+    def close(self) -> None:
+        if self._ctx:
+            self._lib.wcg_close(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int) -> None:
+        self._chk(self._lib.wcg_set_stream(self._ctx, ctypes.c_void_p(stream_ptr)))
+
+    def enable_timing(self, on: bool = True) -> None:
+        self._chk(self._lib.wcg_enable_timing(self._ctx, 1 if on else 0))
+
+    # -- phases
+    def reset(self) -> None:
+        self._chk(self._lib.wcg_reset(self._ctx))
+
+    def map_host(self, data: bytes) -> None:
+        self._chk(self._lib.wcg_map(self._ctx, data, len(data)))
+
+    def map_device(self, dev_ptr: int, n: int) -> None:
+        self._chk(self._lib.wcg_map_device(self._ctx, ctypes.c_void_p(dev_ptr), n))
+
+    def reduce(self) -> Tuple[int, int]:
+        nk, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        self._chk(self._lib.wcg_reduce(self._ctx, ctypes.byref(nk), ctypes.byref(nb)))
+        return nk.value, nb.value
+
+    def result_device(self) -> Tuple[int, int]:
+        p, nb = ctypes.c_void_p(), ctypes.c_uint64()
+        self._chk(self._lib.wcg_result_device(self._ctx, ctypes.byref(p), ctypes.byref(nb)))
+        return p.value or 0, nb.value
+
+    def result(self) -> bytes:
+        _, nb = self.result_device()
+        buf = ctypes.create_string_buffer(max(nb, 1))
+        self._chk(self._lib.wcg_result_copy(self._ctx, buf, nb))
+        return buf.raw[:nb]
+
+    def partition(self, nreduce: int, r: int) -> bytes:
+        nb = ctypes.c_uint64()
+        self._chk(self._lib.wcg_partition(self._ctx, nreduce, r, None, 0, ctypes.byref(nb)))
+        buf = ctypes.create_string_buffer(max(nb.value, 1))
+        self._chk(self._lib.wcg_partition(self._ctx, nreduce, r, buf, nb.value, ctypes.byref(nb)))
+        return buf.raw[:nb.value]
+
+    def export(self, nreduce: int, nranks: int) -> Tuple[int, List[int]]:
+        """Bucket the local aggregate by owner rank; returns (device ptr, units per rank)."""
+        p = ctypes.c_void_p()
+        counts = (ctypes.c_uint64 * nranks)()
+        self._chk(self._lib.wcg_export(self._ctx, nreduce, nranks, ctypes.byref(p), counts))
+        return p.value or 0, list(counts)
+
+    def import_records(self, dev_ptr: int, nunits: int) -> None:
+        self._chk(self._lib.wcg_import(self._ctx, ctypes.c_void_p(dev_ptr), nunits))
+
+    # -- diagnostics
+    def timings(self) -> Tuple[List[float], int]:
+        ms = (ctypes.c_double * 4)()
+        nl = ctypes.c_uint64()
+        self._chk(self._lib.wcg_timings(self._ctx, ms, ctypes.byref(nl)))
+        return list(ms), nl.value
+
+    def stats(self) -> dict:
+        s = (ctypes.c_uint64 * 8)()
+        self._chk(self._lib.wcg_stats(self._ctx, s))
+        keys = ["tokens", "keys", "lds_hits", "global_ops", "long_tokens", "arena_bytes", "overflow",
+                "spin_fail"]
+        return dict(zip(keys, list(s)))
+
+
+def version() -> str:
+    return load().wcg_version().decode()
