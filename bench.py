@@ -124,14 +124,16 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    map_ms = []
+    map_ms, phase_ms = [], []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        map_ms.append(eng.timings()[0][0])
+        ph = eng.timings()[0]
+        map_ms.append(ph["map"])
+        phase_ms.append(ph)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -191,6 +193,7 @@ def main():
         }
         if stats:
             out["stats"] = stats
+        out["phase_ms_avg"] = {k: round(sum(p[k] for p in phase_ms) / len(phase_ms), 4) for k in phase_ms[0]}
         out["verified_vs_oracle"] = verified
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample_mib << 20)

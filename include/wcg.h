@@ -108,9 +108,10 @@ WCG_API int wcg_export(wcg_ctx *ctx, uint32_t nreduce, uint32_t nranks, const vo
 WCG_API int wcg_import(wcg_ctx *ctx, const void *dev_records, uint64_t nrecords);
 
 /* Per-phase device time of the last pipeline run, in milliseconds, measured with HIP events
- * on the context's stream: [0] map kernels (sum over wcg_map* calls since wcg_reset),
- * [1] compaction, [2] sort, [3] format.  Also the number of map kernel launches. */
-WCG_API int wcg_timings(wcg_ctx *ctx, double *ms4, uint64_t *map_launches);
+ * on the context's stream: ms[0] map kernel (tokenize + LDS aggregation, summed over the
+ * wcg_map* calls since wcg_reset), ms[1] miss-log aggregation kernel, ms[2] compaction,
+ * ms[3] sort, ms[4] format.  n = number of doubles the caller provides (<= 5). */
+WCG_API int wcg_timings(wcg_ctx *ctx, double *ms, int n, uint64_t *map_launches);
 /* Enable/disable the event timing above (off by default: it adds event records). */
 WCG_API int wcg_enable_timing(wcg_ctx *ctx, int on);
 

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -15,6 +16,7 @@
 #include "../../include/wcg.h"
 #include "wcg_common.h"
 #include "wcg_map.h"
+#include "wcg_agg.h"
 #include "wcg_reduce.h"
 
 using namespace wcg;
@@ -44,11 +46,15 @@ struct wcg_ctx {
     u32* owner = nullptr;
     u64* d_per_rank = nullptr;                // [2 * 1024]: counts, cursors
     Rec* exp_buf = nullptr; u64 exp_cap = 0;
+    // miss log (k_map -> k_agg)
+    uint4* pool = nullptr; u64 pool_bytes = 0;
+    u32* region_len = nullptr; u64 region_len_cap = 0;
+    u32 nbuckets = 64;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> map_ev;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> map_ev, agg_ev;
     hipEvent_t phase_ev[6] = {};
     bool phase_rec = false;
     u64 map_launches = 0;
@@ -251,7 +257,8 @@ int wcg_close(wcg_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     void* bufs[] = {c->d_in, c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->bh, c->lens,
-                    c->d_scalar, c->d_out, c->d_part, c->owner, c->d_per_rank, c->exp_buf};
+                    c->d_scalar, c->d_out, c->d_part, c->owner, c->d_per_rank, c->exp_buf,
+                    c->pool, c->region_len};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -282,6 +289,7 @@ int wcg_reset(wcg_ctx* c) {
     c->nrec = 0;
     c->out_len = 0;
     c->map_ev.clear();
+    c->agg_ev.clear();
     c->ev_used = 0;
     c->phase_rec = false;
     c->map_launches = 0;
@@ -305,11 +313,53 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     a.ltab = c->ltab; a.lmask = c->lslots - 1;
     a.arena = c->arena; a.arena_cap = c->arena_cap;
     a.st = c->st;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    // miss log: one region per (workgroup, bucket); the whole pool is ~n bytes, enough for
+    // 0.4 entries per token of ordinary text; a full region falls back to the global table
+    const u32 P = c->nbuckets;
+    u64 per_wg_bytes = (u64)a.tiles_per_wg * MAP_TILE;
+    a.region_cap = std::max<u64>(1024, per_wg_bytes / (16ull * P));
+    a.pmask = P - 1;
+    u64 need = grid * P * a.region_cap * sizeof(uint4);
+    if (need > c->pool_bytes) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->pool) HIPCHK(c, hipFree(c->pool));
+        c->pool = nullptr; c->pool_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->pool, need));
+        c->pool_bytes = need;
+    }
+    if (grid * P > c->region_len_cap) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->region_len) HIPCHK(c, hipFree(c->region_len));
+        c->region_len = nullptr; c->region_len_cap = 0;
+        HIPCHK(c, hipMalloc(&c->region_len, grid * P * sizeof(u32)));
+        c->region_len_cap = grid * P;
+    }
+    a.pool = c->pool;
+    a.region_len = c->region_len;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (c->timing) { e0 = take_event(c); HIPCHK(c, hipEventRecord(e0, c->stream)); }
-    k_map<<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a);
+    static const int ablate = getenv("WCG_MAP_ABLATE") ? atoi(getenv("WCG_MAP_ABLATE")) : 0;
+    switch (ablate) {
+        case 1: k_map<1><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
+        case 2: k_map<2><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
+        case 3: k_map<3><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
+        default: k_map<0><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
+    }
     HIPCHK(c, hipGetLastError());
-    if (c->timing) { e1 = take_event(c); HIPCHK(c, hipEventRecord(e1, c->stream)); c->map_ev.push_back({e0, e1}); }
+    if (c->timing) { e1 = take_event(c); HIPCHK(c, hipEventRecord(e1, c->stream)); }
+    AggArgs g;
+    g.pool = c->pool; g.region_len = c->region_len; g.region_cap = a.region_cap;
+    g.P = P; g.nsrc = (u32)grid;
+    g.slices = std::max<u32>(1, std::min<u32>((u32)grid, (u32)(c->ncu + P - 1) / P));
+    g.gtab = c->gtab; g.gmask = c->gslots - 1; g.st = c->st;
+    k_agg<<<P * g.slices, AGG_NT, 0, c->stream>>>(g);
+    HIPCHK(c, hipGetLastError());
+    if (c->timing) {
+        e2 = take_event(c);
+        HIPCHK(c, hipEventRecord(e2, c->stream));
+        c->map_ev.push_back({e0, e1});
+        c->agg_ev.push_back({e1, e2});
+    }
     c->map_launches++;
     c->compacted = c->reduced = false;
     return WCG_OK;
@@ -432,23 +482,21 @@ int wcg_import(wcg_ctx* c, const void* dev_records, uint64_t nrecords) {
     return check_status(c);
 }
 
-int wcg_timings(wcg_ctx* c, double* ms4, uint64_t* map_launches) {
-    if (!c || !ms4) return WCG_EINVAL;
+int wcg_timings(wcg_ctx* c, double* ms, int n, uint64_t* map_launches) {
+    if (!c || !ms || n < 0) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < 4; i++) ms4[i] = 0;
-    for (auto& p : c->map_ev) {
-        float ms = 0;
-        HIPCHK(c, hipEventElapsedTime(&ms, p.first, p.second));
-        ms4[0] += ms;
-    }
+    double v[5] = {0, 0, 0, 0, 0};
+    float f = 0;
+    for (auto& p : c->map_ev) { HIPCHK(c, hipEventElapsedTime(&f, p.first, p.second)); v[0] += f; }
+    for (auto& p : c->agg_ev) { HIPCHK(c, hipEventElapsedTime(&f, p.first, p.second)); v[1] += f; }
     if (c->phase_rec) {
-        float ms = 0;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->phase_ev[0], c->phase_ev[1])); ms4[1] = ms;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->phase_ev[2], c->phase_ev[3])); ms4[2] = ms;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->phase_ev[3], c->phase_ev[4])); ms4[3] = ms;
+        HIPCHK(c, hipEventElapsedTime(&f, c->phase_ev[0], c->phase_ev[1])); v[2] = f;
+        HIPCHK(c, hipEventElapsedTime(&f, c->phase_ev[2], c->phase_ev[3])); v[3] = f;
+        HIPCHK(c, hipEventElapsedTime(&f, c->phase_ev[3], c->phase_ev[4])); v[4] = f;
     }
+    for (int i = 0; i < n && i < 5; i++) ms[i] = v[i];
     if (map_launches) *map_launches = c->map_launches;
     return WCG_OK;
 }

@@ -27,10 +27,25 @@ namespace wcg {
 typedef unsigned long long u64;
 typedef unsigned int u32;
 
-// ---- global aggregation table entry (HBM).  inline keys: k0 = bytes 0-7 (LE),
-// k1 = bytes 8-14 | len << 56 (len 1..15, so k1 != 0 once published); cnt = occurrences.
-// long-key table: k0 = 64-bit hash tag (|1), k1 = arena offset + 1 (publish word),
-// aux = key length.
+// ---- key identity (fact F4), shared by the LDS tables, the miss log and the global table:
+//   len <= 7 : k0 = key bytes 0..len-1 (little-endian, zero padded) | len << 56, k1 = 0
+//   len 8-15 : k0 = key bytes 0-7, k1 = key bytes 8..len-1 (zero padded) | len << 56
+// Byte 7 of a key of 8+ bytes is a letter byte (>= 0x41), so k0 >> 56 < 8 identifies short
+// keys and one 64-bit compare decides equality for them (89% of tokens of the C2 corpus).
+// k0 is never 0 and k1 is never 0 for keys of 8+ bytes.
+__device__ __forceinline__ bool key_short(u64 k0) { return (k0 >> 56) < 8; }
+__device__ __forceinline__ int key_len(u64 k0, u64 k1) {
+    u32 t = (u32)(k0 >> 56);
+    return t < 8 ? (int)t : (int)(k1 >> 56);
+}
+// raw little-endian key bytes -> identity (b0/b1 already hold only the key's bytes)
+__device__ __forceinline__ void make_key(u64 b0, u64 b1, int len, u64& k0, u64& k1) {
+    if (len <= 7) { k0 = b0 | (u64)len << 56; k1 = 0; }
+    else { k0 = b0; k1 = b1 | (u64)len << 56; }
+}
+
+// ---- global aggregation table entry (HBM): inline keys {k0, k1, cnt}; the long-key table
+// uses k0 = 64-bit hash tag (|1), k1 = arena offset + 1 (publish word), aux = key length.
 struct __align__(32) GEntry { u64 k0, k1, cnt, aux; };
 
 // ---- sorted record (after compaction): the 128-bit big-endian prefix is the sort key.
@@ -123,8 +138,18 @@ __device__ __host__ __forceinline__ u64 mix64(u64 x) {
     x ^= x >> 32; x *= 0xD6E8FEB86659FD93ull; x ^= x >> 32; x *= 0xD6E8FEB86659FD93ull; x ^= x >> 32;
     return x;
 }
+// 64-bit key hash: miss-log bucket and global-table slot (computed off the hit path)
 __device__ __forceinline__ u64 key_hash(u64 k0, u64 k1) {
     return mix64(k0 * 0x9E3779B97F4A7C15ull + (k1 ^ (k1 >> 29)) * 0xC2B2AE3D27D4EB4Full);
+}
+// 32-bit key hash for the LDS tables (two 32-bit multiplies on the hot path)
+__device__ __forceinline__ u32 lds_hash(u64 k0, u64 k1) {
+    u32 x = (u32)k0 ^ __builtin_rotateleft32((u32)(k0 >> 32), 11) ^ __builtin_rotateleft32((u32)k1, 19) ^
+            __builtin_rotateleft32((u32)(k1 >> 32), 27);
+    x ^= x >> 16; x *= 0x7FEB352Du;
+    x ^= x >> 15; x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
 }
 __device__ __forceinline__ u32 fnv1a_step(u32 h, u32 byte) { return (h ^ byte) * 0x01000193u; }
 
@@ -152,27 +177,29 @@ __device__ __forceinline__ void add_agent(u64* p, u64 v) {
 
 constexpr int SPIN_LIMIT = 1 << 20;
 
-// Insert/accumulate an inline key into the global table (open addressing, linear probing).
-// Claim protocol: CAS k0 0->key, then publish k1 (never 0 for a valid key).  A reader that
-// sees k0 == key but k1 == 0 re-reads in a later iteration (the claimer publishes in the same
-// iteration of its own loop, so no lane waits on a lane parked behind it).
-__device__ __forceinline__ void ginsert(GEntry* tab, u64 mask, u64 k0, u64 k1, u64 h, u64 cnt, DevState* st) {
-    u64 s = h & mask;
+// Insert/accumulate an inline key into the global table (open addressing, linear probing from
+// slot_hash).  Claim protocol: CAS k0 0 -> key; a key of 8+ bytes then publishes k1 (never 0).
+// A reader that sees k0 == key but k1 == 0 re-reads in a later iteration (the claimer publishes
+// in the same iteration of its own loop, so no lane waits on a lane parked behind it).
+__device__ __forceinline__ void ginsert(GEntry* tab, u64 mask, u64 k0, u64 k1, u64 slot_hash, u64 cnt, DevState* st) {
+    u64 s = slot_hash & mask;
     u64 probes = 0;
     int spins = 0;
+    const bool shrt = key_short(k0);
     while (true) {
         GEntry* e = &tab[s];
         u64 c0 = ld_agent(&e->k0);
         if (c0 == 0) {
             u64 exp = 0;
             if (cas_agent(&e->k0, &exp, k0)) {
-                st_agent(&e->k1, k1);
+                if (!shrt) st_agent(&e->k1, k1);
                 add_agent(&e->cnt, cnt);
                 return;
             }
             c0 = exp;
         }
         if (c0 == k0) {
+            if (shrt) { add_agent(&e->cnt, cnt); return; }
             u64 c1 = ld_agent(&e->k1);
             if (c1 == k1) { add_agent(&e->cnt, cnt); return; }
             if (c1 == 0) {                                   // claimed, not yet published

@@ -10,6 +10,7 @@
 //               {"Key":"k","Value":"count"}\n for ihash(k)%R == r (DoReduce, :274-278)
 #pragma once
 #include "wcg_common.h"
+#include "wcg_lds_table.h"
 
 namespace wcg {
 
@@ -28,10 +29,16 @@ __global__ void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u6
             GEntry e = gtab[i];
             if (e.k0 != 0) {
                 have = true;
-                r.hi = bswap64(e.k0);
-                r.lo = bswap64(e.k1 & 0x00FFFFFFFFFFFFFFull);
+                if (key_short(e.k0)) {
+                    r.hi = bswap64(e.k0 & 0x00FFFFFFFFFFFFFFull);
+                    r.lo = 0;
+                    r.ref = e.k0 >> 56;
+                } else {
+                    r.hi = bswap64(e.k0);
+                    r.lo = bswap64(e.k1 & 0x00FFFFFFFFFFFFFFull);
+                    r.ref = e.k1 >> 56;
+                }
                 r.cnt = e.cnt;
-                r.ref = e.k1 >> 56;
             }
         } else if (i < total) {
             GEntry e = ltab[i - gslots];
@@ -345,8 +352,9 @@ __global__ void k_import(const Rec* in, u64 n, GEntry* gtab, u64 gmask, GEntry* 
         Rec x = in[i];
         if (x.ref == CONT_MARK) continue;
         if (!(x.ref & LONG_FLAG)) {
-            u64 k0 = bswap64(x.hi), k1 = bswap64(x.lo) | (x.ref << 56);
-            ginsert(gtab, gmask, k0, k1, key_hash(k0, k1), x.cnt, st);
+            u64 k0, k1;
+            make_key(bswap64(x.hi), bswap64(x.lo), (int)x.ref, k0, k1);
+            ginsert(gtab, gmask, k0, k1, gslot(key_hash(k0, k1)), x.cnt, st);
             continue;
         }
         u64 len = (x.ref >> 40) & LONG_LEN_MAX;

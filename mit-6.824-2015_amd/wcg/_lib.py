@@ -57,7 +57,7 @@ def load() -> ctypes.CDLL:
         "wcg_partition": (I, [P, U32, U32, P, U64, PU64]),
         "wcg_export": (I, [P, U32, U32, ctypes.POINTER(P), PU64]),
         "wcg_import": (I, [P, P, U64]),
-        "wcg_timings": (I, [P, ctypes.POINTER(ctypes.c_double), PU64]),
+        "wcg_timings": (I, [P, ctypes.POINTER(ctypes.c_double), I, PU64]),
         "wcg_enable_timing": (I, [P, I]),
         "wcg_stats": (I, [P, PU64]),
         "wcg_ihash": (U32, [ctypes.c_char_p, U64]),
@@ -166,11 +166,14 @@ class Engine:
         self._chk(self._lib.wcg_import(self._ctx, ctypes.c_void_p(dev_ptr), nunits))
 
     # -- diagnostics
-    def timings(self) -> Tuple[List[float], int]:
-        ms = (ctypes.c_double * 4)()
+    PHASES = ("map", "agg", "compact", "sort", "format")
+
+    def timings(self) -> Tuple[dict, int]:
+        """Device ms per phase of the last job (needs enable_timing) and map launch count."""
+        ms = (ctypes.c_double * 5)()
         nl = ctypes.c_uint64()
-        self._chk(self._lib.wcg_timings(self._ctx, ms, ctypes.byref(nl)))
-        return list(ms), nl.value
+        self._chk(self._lib.wcg_timings(self._ctx, ms, 5, ctypes.byref(nl)))
+        return dict(zip(self.PHASES, list(ms))), nl.value
 
     def stats(self) -> dict:
         s = (ctypes.c_uint64 * 8)()

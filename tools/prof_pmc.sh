@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC passes (each its own run, --pmc only with kernel filtering; no sys/runtime trace) over a
+# short bench run.  Usage: tools/prof_pmc.sh OUTDIR KERNEL_REGEX [bench args...]
+export TMPDIR=/tmp
+OUT=$1; KRE=$2; shift 2
+passes=(
+ "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU"
+ "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH SQ_WAVES GRBM_GUI_ACTIVE"
+ "FETCH_SIZE"
+ "WRITE_SIZE"
+)
+i=0
+for p in "${passes[@]}"; do
+  i=$((i+1))
+  rocprofv3 --pmc $p --kernel-include-regex "$KRE" --output-format csv -d "$OUT/pass$i" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify "$@" || exit $?
+done
