@@ -305,10 +305,10 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     MapArgs a;
     a.in = (const uint8_t*)dev_bytes;
     a.n = n;
-    a.ntiles = (n + MAP_TILE - 1) / MAP_TILE;
-    u64 grid = std::min<u64>((u64)c->ncu, a.ntiles);
-    a.tiles_per_wg = (a.ntiles + grid - 1) / grid;
-    grid = (a.ntiles + a.tiles_per_wg - 1) / a.tiles_per_wg;
+    a.ntiles = (n + MAP_STEP - 1) / MAP_STEP;      // 1 KiB wave steps
+    // one workgroup per CU (LDS-bound); steps are dealt chip-wide inside the kernel
+    u64 grid = std::min<u64>((u64)c->ncu, (a.ntiles + MAP_WAVES - 1) / MAP_WAVES);
+    a.tiles_per_wg = (a.ntiles + grid - 1) / grid;          // steps per workgroup (sizing only)
     a.gtab = c->gtab; a.gmask = c->gslots - 1;
     a.ltab = c->ltab; a.lmask = c->lslots - 1;
     a.arena = c->arena; a.arena_cap = c->arena_cap;
@@ -316,7 +316,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // miss log: one region per (workgroup, bucket); the whole pool is ~n bytes, enough for
     // 0.4 entries per token of ordinary text; a full region falls back to the global table
     const u32 P = c->nbuckets;
-    u64 per_wg_bytes = (u64)a.tiles_per_wg * MAP_TILE;
+    u64 per_wg_bytes = (u64)a.tiles_per_wg * MAP_STEP;
     a.region_cap = std::max<u64>(1024, per_wg_bytes / (16ull * P));
     a.pmask = P - 1;
     u64 need = grid * P * a.region_cap * sizeof(uint4);
@@ -343,6 +343,8 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         case 1: k_map<1><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
         case 2: k_map<2><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
         case 3: k_map<3><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
+        case 4: k_map<4><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
+        case 5: k_map<5><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
         default: k_map<0><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
     }
     HIPCHK(c, hipGetLastError());

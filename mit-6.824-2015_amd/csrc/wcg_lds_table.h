@@ -41,37 +41,50 @@ struct LdsTable {
         v[2] = (u64)y.y << 32 | y.x; v[3] = (u64)y.w << 32 | y.z;
     }
 
-    // aggregate (key, c) with h = lds_hash(key); false when both buckets hold other keys
+    // aggregate (key, c) with h = lds_hash(key); false when both buckets hold other keys.
+    // Straight-line common path: both buckets are read, the 8 candidate slots become bit
+    // masks (slot s: bucket s >> 2, way s & 3), one LDS atomic at a computed address.
     __device__ __forceinline__ bool add(u64 a0, u64 a1, u32 h, CNT c) {
         u32 b1, b2;
         buckets(h, b1, b2);
         const bool shrt = key_short(a0);
-        u64 v[4];
+        u64 v[4], w[4];
         read4(b1, v);
-        // common case: the key sits in its first bucket
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (v[j] == a0 && (shrt || k1[b1][j] == a1)) { add_cnt(b1, j, c); return true; }
-        u64 w[4];
         read4(b2, w);
+        u32 m = 0, e = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (w[j] == a0 && (shrt || k1[b2][j] == a1)) { add_cnt(b2, j, c); return true; }
-        // insert into the first empty slot of b1, then b2
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const u32 b = q ? b2 : b1;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                if ((q ? w[j] : v[j]) != 0) continue;
-                u64 old = atomicCAS(&k0[b][j], 0ull, a0);
-                if (old == 0) {
-                    if (!shrt) k1[b][j] = a1;
-                    add_cnt(b, j, c);
-                    return true;
-                }
-                if (old == a0 && (shrt || k1[b][j] == a1)) { add_cnt(b, j, c); return true; }
+        for (int j = 0; j < 4; j++) {
+            m |= (u32)(v[j] == a0) << j;
+            m |= (u32)(w[j] == a0) << (4 + j);
+            e |= (u32)(v[j] == 0) << j;
+            e |= (u32)(w[j] == 0) << (4 + j);
+        }
+        if (!shrt && m) {                       // keys of 8+ bytes: confirm k1 (usually 1 candidate)
+            u32 mm = m;
+            m = 0;
+            while (mm) {
+                const int s = __ffs(mm) - 1;
+                mm &= mm - 1;
+                if (k1[s < 4 ? b1 : b2][s & 3] == a1) { m = 1u << s; break; }
             }
+        }
+        if (m) {
+            const int s = __ffs(m) - 1;
+            add_cnt(s < 4 ? b1 : b2, s & 3, c);
+            return true;
+        }
+        while (e) {                             // insert: first empty slot of b1, then b2
+            const int s = __ffs(e) - 1;
+            e &= e - 1;
+            const u32 b = s < 4 ? b1 : b2;
+            const int j = s & 3;
+            const u64 old = atomicCAS(&k0[b][j], 0ull, a0);
+            if (old == 0) {
+                if (!shrt) k1[b][j] = a1;
+                add_cnt(b, j, c);
+                return true;
+            }
+            if (old == a0 && (shrt || k1[b][j] == a1)) { add_cnt(b, j, c); return true; }
         }
         return false;
     }

@@ -1,34 +1,65 @@
 // wcg_map.h - the map kernel: DoMap + Map (mapreduce.go:193-231, wc.go:17-30) on gfx950.
 //
-// One workgroup (16 waves) per CU walks a contiguous range of tiles (TILE = NT * 16 bytes):
-//   1. every thread loads one 16-byte chunk (coalesced dwordx4; the next tile is prefetched
-//      into registers while the current one is processed), plus a 16-byte prefix and a
-//      64-byte look-ahead so tokens that cross the tile end can be read whole;
-//   2. per chunk: 16-bit letter-byte mask - SWAR on all-ASCII chunks, Go UTF-8 decode +
-//      Unicode-13 letter bitmap otherwise;
-//   3. token starts = letter & ~prev_letter; each wave compacts its starts (ballot/mbcnt
-//      prefix sum, no LDS shuffles) into an LDS list and processes them 64 at a time;
-//   4. per token: length from the LDS mask, key identity (<= 15 bytes, fact F4) -> LDS hash
-//      table (exact keys, 2-choice x 4-way buckets, u32 counts); an LDS miss is appended to
-//      this workgroup's region of the miss log (plain stores, no atomics) for k_agg; tokens
-//      > 15 bytes go to the long-key table with an arena copy of their bytes;
-//   5. at the end of its range the workgroup flushes its LDS table into the miss log too.
-// Token ownership: a token belongs to the tile holding its first byte (counted exactly once).
+// One workgroup (16 waves) per CU owns a contiguous range of 1 KiB steps; wave w of the
+// workgroup processes steps w, w+16, w+32, ... of that range on its own - its own LDS slice,
+// no workgroup barrier in the main loop, so the 16 waves overlap each other's latencies:
+//   1. every lane loads one 16-byte chunk of the step (one coalesced 1 KiB dwordx4 load per
+//      wave), lanes 0-4 also the 16-byte prefix and the 64-byte look-ahead that lets tokens
+//      crossing the step end be read whole; the loads run 2 steps ahead in registers;
+//   2. per chunk: 16-bit letter-byte mask - SWAR on all-ASCII chunks (fact F2), Go UTF-8
+//      decode + Unicode-13 letter bitmap otherwise (fact F1);
+//   3. token starts = letter & ~prev_letter (fact F3); the wave compacts them (prefix sum from
+//      4 ballots + mbcnt) into its LDS list and processes them 64 at a time;
+//   4. per token: length from the mask, key identity (<= 15 bytes, fact F4) -> the
+//      workgroup's LDS hash table (exact keys, 2-choice x 4-way buckets, u32 counts); an LDS
+//      miss is appended to this workgroup's region of the miss log (plain stores) for k_agg;
+//      tokens > 15 bytes go to the long-key table with an arena copy of their bytes;
+//   5. at the end the workgroup flushes its LDS table into the miss log too.
+// Token ownership: a token belongs to the 16-byte chunk holding its first byte (exactly once).
 #pragma once
 #include "wcg_common.h"
 #include "wcg_lds_table.h"
 
 namespace wcg {
 
-constexpr int MAP_NT = 1024;                 // threads per workgroup (16 waves)
-constexpr int MAP_TILE = MAP_NT * 16;        // bytes per tile
+constexpr int MAP_NT = 1024;                 // threads per workgroup
+constexpr int MAP_WAVES = MAP_NT / 64;       // 16 independent waves
+constexpr int MAP_STEP = 1024;               // bytes per wave step (64 lanes x 16 B)
 constexpr int MAP_PRE = 16;                  // prefix bytes (need 4)
 constexpr int MAP_LOOK = 64;                 // look-ahead bytes (tokens <= 15 need 15)
-constexpr int MAP_REG = MAP_PRE + MAP_TILE + MAP_LOOK;
-constexpr int MAP_NCH = MAP_REG / 16;        // chunks in the LDS region
-constexpr int MAP_WAVES = MAP_NT / 64;
-constexpr int MAP_NB = 1584;                 // LDS table buckets (x4 slots, 20 B per slot)
+constexpr int MAP_WREG = MAP_PRE + MAP_STEP + MAP_LOOK;   // 1104 = 69 chunks
+constexpr int MAP_WNCH = MAP_WREG / 16;
+constexpr int MAP_WMASK = 72;                // mask slots per wave (69 + padding)
+constexpr int MAP_NB = 1576;                 // LDS table buckets (x4 slots, 20 B per slot)
 constexpr int MAX_MISS_BUCKETS = 256;
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// Streaming input loads are inline-asm buffer loads with hand-counted waits: the compiler's
+// waitcnt pass drains every load (vmcnt(0)) at the top of this loop, which serialises the
+// prefetch.  Rules kept here: each wait names its registers as "+v" so no use moves above it,
+// every asm-loaded register is waited for before it can die or be copied, and N counts only
+// this wave's own younger asm loads (compiler-issued memory ops in between can only make a
+// wait stronger).
+__device__ __forceinline__ v4u buf_load16(v4i rsrc, u32 off) {
+    v4u r;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=&v"(r) : "v"(off), "s"(rsrc) : "memory");
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void buf_wait(v4u& x, v4u& y) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(x), "+v"(y) : "n"(N) : "memory");
+}
+__device__ __forceinline__ v4i make_rsrc(const void* base, u32 nbytes) {
+    const u64 p = (u64)base;
+    v4i r;
+    r.x = __builtin_amdgcn_readfirstlane((int)(u32)p);
+    r.y = __builtin_amdgcn_readfirstlane((int)((u32)(p >> 32) & 0xFFFFu));
+    r.z = __builtin_amdgcn_readfirstlane((int)nbytes);
+    r.w = 0x00020000;
+    return r;
+}
 
 struct MapArgs {
     const uint8_t* in;
@@ -125,145 +156,183 @@ __device__ void long_token(const MapArgs& a, u64 p) {
 }
 
 // ABL (measurement builds only, selected by WCG_MAP_ABLATE; results are wrong when ABL != 0):
-//   1 = tokenize + compact only, 2 = + key extraction and hash, 3 = + LDS lookup, misses dropped
+//   5 = input loads only, 4 = + LDS staging and letter masks, 1 = + token starts and compaction,
+//   2 = + key extraction and hash, 3 = + LDS lookup with misses dropped
 template <int ABL>
 __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
-    __shared__ __align__(16) uint8_t sbytes[MAP_REG];
-    __shared__ __align__(16) uint16_t smask[MAP_NCH + 8];
-    __shared__ uint16_t sstart[MAP_WAVES][512];
+    __shared__ __align__(16) uint8_t wbytes[MAP_WAVES][MAP_WREG];
+    __shared__ __align__(16) uint16_t wmask[MAP_WAVES][MAP_WMASK];
+    __shared__ uint16_t wstart[MAP_WAVES][512];
     __shared__ __align__(16) u64 tk0[MAP_NB][4];
     __shared__ __align__(16) u64 tk1[MAP_NB][4];
     __shared__ u32 tcnt[MAP_NB][4];
     __shared__ u32 cursor[MAX_MISS_BUCKETS];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);     // wave-uniform (scalar)
     LdsTable<MAP_NB, u32> tab{tk0, tk1, tcnt};
     tab.init(tid, MAP_NT);
     for (int i = tid; i < MAX_MISS_BUCKETS; i += MAP_NT) cursor[i] = 0;
-    if (tid < 8) smask[MAP_NCH + tid] = 0;
-
-    const u64 t0 = (u64)blockIdx.x * a.tiles_per_wg;
-    u64 t1 = t0 + a.tiles_per_wg;
-    if (t1 > a.ntiles) t1 = a.ntiles;
-
-    // chunk c of the region <-> input bytes [base - PRE + 16c, +16)
-    // thread tid owns chunk tid+1; threads 0..4 also own chunk 0 and chunks NT+1..NT+4
-    const int xc = (tid == 0) ? 0 : (tid <= 4 ? MAP_NT + tid : -1);
-    uint4 cur = make_uint4(0, 0, 0, 0), curx = cur;
-    if (t0 < t1) {
-        long base = (long)(t0 * MAP_TILE);
-        cur = load_chunk(a.in, a.n, base - MAP_PRE + 16 * (tid + 1));
-        if (xc >= 0) curx = load_chunk(a.in, a.n, base - MAP_PRE + 16 * xc);
-    }
-    u64 my_tokens = 0, my_hits = 0, my_global = 0, my_long = 0;
+    if (lane < MAP_WMASK - MAP_WNCH) wmask[wave][MAP_WNCH + lane] = 0;
     __syncthreads();
 
-    for (u64 t = t0; t < t1; t++) {
-        const long base = (long)(t * MAP_TILE);
-        // ---- stage the tile in LDS, prefetch the next one into registers
-        reinterpret_cast<uint4*>(sbytes)[tid + 1] = cur;
-        if (xc >= 0) reinterpret_cast<uint4*>(sbytes)[xc] = curx;
-        const uint4 mine = cur;
-        if (t + 1 < t1) {
-            long nb = base + MAP_TILE;
-            cur = load_chunk(a.in, a.n, nb - MAP_PRE + 16 * (tid + 1));
-            if (xc >= 0) curx = load_chunk(a.in, a.n, nb - MAP_PRE + 16 * xc);
-        }
-        __syncthreads();
+    uint8_t* const bytes = wbytes[wave];
+    uint16_t* const msk = wmask[wave];
+    uint16_t* const sst = wstart[wave];
+    // Steps are dealt chip-wide: wave w of workgroup g takes steps (g * 16 + w) + k * G * 16, so
+    // the chip sweeps the input front to back (HBM-friendly) while every workgroup still sees
+    // a uniform sample of it for its LDS table.
+    const u64 nsteps = a.ntiles;
+    const u64 stride = (u64)gridDim.x * MAP_WAVES;
+    // region chunk c <-> input bytes [step_base - PRE + 16c, +16): lane owns chunk lane+1,
+    // lane 0 also chunk 0 (prefix), lanes 1-4 also chunks 65-68 (look-ahead)
+    const int xc = (lane == 0) ? 0 : (lane <= 4 ? 64 + lane : -1);
+    u64 my_tokens = 0, my_hits = 0, my_global = 0, my_long = 0;
 
-        // ---- letter masks (fact F2: an all-ASCII chunk needs no context)
-        auto at = [&](long i) -> u32 { return (i >= 0 && i < MAP_REG) ? (u32)sbytes[i] : 0u; };
+    // Input loads: raw buffer loads through a per-step descriptor based at the step's prefix
+    // (at the input start for step 0); the hardware range check returns zeros for the prefix
+    // of step 0 and past the end.  Every prefetch is unconditional (the waitcnt pass can only
+    // count younger loads that are certainly issued): lanes without an extra chunk and steps
+    // past the end load offset 0xFFFFFFF0, which reads zeros without touching memory.
+    auto load = [&](u64 step, v4u& m, v4u& x) {
+        const bool live = step < nsteps;
+        const u64 org = (step == 0 || !live) ? 0 : step * MAP_STEP - MAP_PRE;
+        const u64 span = live ? a.n - org : 0;
+        const u32 nrec = span > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)span;
+        const v4i rsrc = make_rsrc(a.in + org, nrec);
+        const u32 rel = (u32)(step * MAP_STEP - org);            // 0 for step 0, else 16
+        const u32 om = live ? rel + 16 * lane : 0xFFFFFFF0u;
+        const u32 ox = (live && xc >= 0) ? rel - MAP_PRE + 16 * xc : 0xFFFFFFF0u;
+        m = buf_load16(rsrc, om);
+        x = buf_load16(rsrc, ox);
+    };
+
+    auto process = [&](u64 step, const uint4 mine, const uint4 extra) {
+        const long base = (long)(step * MAP_STEP);
+        if (ABL == 5) { asm volatile("" ::"v"(mine.x ^ extra.y)); return; }
+        reinterpret_cast<uint4*>(bytes)[lane + 1] = mine;
+        if (xc >= 0) reinterpret_cast<uint4*>(bytes)[xc] = extra;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- letter masks
+        auto at = [&](long i) -> u32 { return (i >= 0 && i < MAP_WREG) ? (u32)bytes[i] : 0u; };
         {
-            const int ch = tid + 1;
             u32 m;
             if (all_ascii(mine)) {
                 m = ascii_mask16(mine);
             } else {
                 m = 0;
                 for (int i = 0; i < 16; i++)
-                    if (letter_byte(at, (long)(16 * ch + i))) m |= 1u << i;
+                    if (letter_byte(at, (long)(16 * (lane + 1) + i))) m |= 1u << i;
             }
-            smask[ch] = (uint16_t)m;
+            msk[lane + 1] = (uint16_t)m;
             if (xc >= 0) {
-                uint4 v = reinterpret_cast<const uint4*>(sbytes)[xc];
-                if (all_ascii(v)) {
-                    m = ascii_mask16(v);
+                if (all_ascii(extra)) {
+                    m = ascii_mask16(extra);
                 } else {
                     m = 0;
-                    for (int i = (xc == 0 ? 4 : 0); i < 16; i++)      // prefix chunk: only its tail matters
+                    for (int i = (xc == 0 ? 4 : 0); i < 16; i++)   // prefix chunk: only its tail matters
                         if (letter_byte(at, (long)(16 * xc + i))) m |= 1u << i;
                 }
-                smask[xc] = (uint16_t)m;
+                msk[xc] = (uint16_t)m;
             }
         }
-        __syncthreads();
-
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (ABL == 4) { asm volatile("" ::"v"((u32)msk[lane + 1])); return; }
         // ---- token starts in my chunk; wave prefix sum of the counts (<= 8) from 4 ballots
-        {
-            const int ch = tid + 1;
-            const u32 m = smask[ch];
-            const u32 prev = smask[ch - 1] >> 15;
-            u32 starts = m & ~((m << 1) | prev) & 0xFFFFu;
-            const u32 cnt = __popc(starts);
-            u32 o = 0, total = 0;
+        const u32 m = msk[lane + 1];
+        const u32 prev = msk[lane] >> 15;
+        u32 starts = m & ~((m << 1) | prev) & 0xFFFFu;
+        const u32 cnt = __popc(starts);
+        u32 o = 0, total = 0;
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const u64 bal = __ballot((cnt >> b) & 1);
-                o += __builtin_amdgcn_mbcnt_hi((u32)(bal >> 32), __builtin_amdgcn_mbcnt_lo((u32)bal, 0u)) << b;
-                total += (u32)__popcll(bal) << b;
-            }
-            while (starts) {
-                const int b = __ffs(starts) - 1;
-                starts &= starts - 1;
-                sstart[wave][o++] = (uint16_t)(16 * (ch - 1) + b);   // tile-relative offset
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            my_tokens += (lane == 0) ? (u64)total : 0;
-
-            u32 sink = 0;
-            for (u32 i = lane; i < total; i += 64) {
-                if (ABL == 1) { sink += sstart[wave][i]; continue; }
-                const int off = sstart[wave][i];
-                const int rp = MAP_PRE + off;                       // region position
-                const int wi = rp >> 4, bi = rp & 15;
-                const u32 w32 = (u32)smask[wi] | ((u32)smask[wi + 1] << 16);
-                const u32 v = ~(w32 >> bi);                         // >= 17 valid bits
-                const int len = v ? __ffs(v) - 1 : 32;              // v == 0: run covers the window
-                if (len >= 16) {
-                    my_long++;
-                    long_token(a, (u64)(base + off));
-                    continue;
-                }
-                // key bytes [rp, rp+16) from LDS via 5 aligned dwords
-                const int al = rp & ~3, sh = rp & 3;
-                const u32* d = reinterpret_cast<const u32*>(sbytes + al);
-                const u32 d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
-                const u32 o0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-                const u32 o1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-                const u32 o2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-                const u32 o3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-                const u64 b0 = ((u64)o1 << 32 | o0) & low_bytes_mask(len);
-                const u64 b1 = len > 8 ? (((u64)o3 << 32 | o2) & low_bytes_mask(len - 8)) : 0ull;
-                u64 k0, k1;
-                make_key(b0, b1, len, k0, k1);
-                if (ABL == 2) { sink += lds_hash(k0, k1); continue; }
-                if (ABL == 3) { sink += tab.add(k0, k1, lds_hash(k0, k1), 1u); continue; }
-                if (tab.add(k0, k1, lds_hash(k0, k1), 1u)) {
-                    my_hits++;
-                } else {
-                    const u64 h2 = key_hash(k0, k1);
-                    if (!log_push(a, cursor, miss_bucket(h2, a.pmask), entry(k0, k1))) {
-                        my_global++;
-                        ginsert(a.gtab, a.gmask, k0, k1, gslot(h2), 1, a.st);
-                    }
-                }
-            }
-            if (ABL) asm volatile("" ::"v"(sink));
+        for (int b = 0; b < 4; b++) {
+            const u64 bal = __ballot((cnt >> b) & 1);
+            o += __builtin_amdgcn_mbcnt_hi((u32)(bal >> 32), __builtin_amdgcn_mbcnt_lo((u32)bal, 0u)) << b;
+            total += (u32)__popcll(bal) << b;
         }
-        __syncthreads();
+        while (starts) {
+            const int b = __ffs(starts) - 1;
+            starts &= starts - 1;
+            sst[o++] = (uint16_t)(16 * lane + b);               // step-relative offset
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        my_tokens += (lane == 0) ? (u64)total : 0;
+
+        u32 sink = 0;
+        for (u32 i = lane; i < total; i += 64) {
+            if (ABL == 1) { sink += sst[i]; continue; }
+            const int off = sst[i];
+            const int rp = MAP_PRE + off;                       // region position
+            const int wi = rp >> 4, bi = rp & 15;
+            const u32 w32 = (u32)msk[wi] | ((u32)msk[wi + 1] << 16);
+            const u32 v = ~(w32 >> bi);                         // >= 17 valid bits
+            const int len = v ? __ffs(v) - 1 : 32;              // v == 0: run covers the window
+            if (len >= 16) {
+                my_long++;
+                long_token(a, (u64)(base + off));
+                continue;
+            }
+            // key bytes [rp, rp+16) from LDS via 5 aligned dwords
+            const int al = rp & ~3, sh = rp & 3;
+            const u32* d = reinterpret_cast<const u32*>(bytes + al);
+            const u32 d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+            const u32 o0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            const u32 o1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            const u32 o2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+            const u32 o3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+            const u64 b0 = ((u64)o1 << 32 | o0) & low_bytes_mask(len);
+            const u64 b1 = len > 8 ? (((u64)o3 << 32 | o2) & low_bytes_mask(len - 8)) : 0ull;
+            u64 k0, k1;
+            make_key(b0, b1, len, k0, k1);
+            if (ABL == 2) { sink += lds_hash(k0, k1); continue; }
+            if (ABL == 3) { sink += tab.add(k0, k1, lds_hash(k0, k1), 1u); continue; }
+            if (tab.add(k0, k1, lds_hash(k0, k1), 1u)) {
+                my_hits++;
+            } else {
+                const u64 h2 = key_hash(k0, k1);
+                if (!log_push(a, cursor, miss_bucket(h2, a.pmask), entry(k0, k1))) {
+                    my_global++;
+                    ginsert(a.gtab, a.gmask, k0, k1, gslot(h2), 1, a.st);
+                }
+            }
+        }
+        if (ABL) asm volatile("" ::"v"(sink));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+
+    // two steps in flight per wave (A/B register sets, no copies between them); the step(s)
+    // reaching past the input end are reloaded byte-exactly (cold, separate call site)
+    auto is_tail = [&](u64 step) { return step * MAP_STEP + MAP_STEP + MAP_LOOK > a.n; };
+    auto tail_chunk = [&](u64 step, int c) -> uint4 {
+        return load_chunk(a.in, a.n, (long)(step * MAP_STEP) - MAP_PRE + 16 * c);
+    };
+    auto u4 = [](v4u v) { return make_uint4(v.x, v.y, v.z, v.w); };
+    v4u ma, xa, mb, xb;
+    u64 st = (u64)blockIdx.x * MAP_WAVES + wave;
+    load(st, ma, xa);
+    load(st + stride, mb, xb);
+    for (; st < nsteps; st += 2 * stride) {
+        buf_wait<2>(ma, xa);                     // younger: B's two loads
+        if (is_tail(st)) process(st, tail_chunk(st, lane + 1), xc >= 0 ? tail_chunk(st, xc) : u4(xa));
+        else process(st, u4(ma), u4(xa));
+        load(st + 2 * stride, ma, xa);
+        buf_wait<2>(mb, xb);                     // younger: A's two loads
+        const u64 sb = st + stride;
+        if (sb >= nsteps) break;
+        if (is_tail(sb)) process(sb, tail_chunk(sb, lane + 1), xc >= 0 ? tail_chunk(sb, xc) : u4(xb));
+        else process(sb, u4(mb), u4(xb));
+        load(st + 3 * stride, mb, xb);
     }
+    buf_wait<0>(ma, xa);                         // nothing may land in a dead register
+    buf_wait<0>(mb, xb);
 
     // ---- flush the LDS table into this workgroup's miss-log regions (count 1: one entry,
     //      count c > 1: {k0, k1|CNT_FLAG} + carrier {0, c}); a full region -> global table
