@@ -35,9 +35,9 @@ struct wcg_ctx {
     DevState* h_st = nullptr;                 // pinned mirror
     Rec* recA = nullptr; Rec* recB = nullptr; u64 rec_cap = 0;
     Rec* sorted = nullptr;
-    u32* bh = nullptr; u64 bh_cap = 0;
     u64* lens = nullptr;
     u64* d_scalar = nullptr;                  // scan totals
+    u64* h_scalar = nullptr;                  // pinned mirror of d_scalar[0]
     uint8_t* d_out = nullptr; u64 out_cap = 0; u64 out_len = 0;
     uint8_t* d_part = nullptr; u64 part_cap = 0;
     u64 nrec = 0;
@@ -47,7 +47,7 @@ struct wcg_ctx {
     u64* d_per_rank = nullptr;                // [2 * 1024]: counts, cursors
     Rec* exp_buf = nullptr; u64 exp_cap = 0;
     // miss log (k_map -> k_agg)
-    uint4* pool = nullptr; u64 pool_bytes = 0;
+    u64* pool = nullptr; u64 pool_bytes = 0;
     u32* region_len = nullptr; u64 region_len_cap = 0;
     u32 nbuckets = 64;
     // timing
@@ -101,7 +101,7 @@ hipEvent_t take_event(wcg_ctx* c) {
 }
 
 int check_status(wcg_ctx* c) {
-    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, offsetof(DevState, hist), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->h_st->overflow || c->h_st->spin_fail) {
         char buf[256];
@@ -128,11 +128,11 @@ int ensure(wcg_ctx* c, uint8_t** p, u64* cap, u64 need) {
 
 int compact(wcg_ctx* c) {
     if (c->compacted) return WCG_OK;
-    HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, sizeof(u64), c->stream));
+    HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));   // nrec, nlong
     if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
     u64 total = c->gslots + c->lslots;
-    k_compact<<<grid_for(total, 256, c->ncu * 16), 256, 0, c->stream>>>(c->gtab, c->gslots, c->ltab, c->lslots,
-                                                                       c->arena, c->recA, c->st);
+    k_compact<<<(unsigned)((total + CP_NT * CP_IPT - 1) / (CP_NT * CP_IPT)), CP_NT, 0, c->stream>>>(
+        c->gtab, c->gslots, c->ltab, c->lslots, c->arena, c->recA, c->st);
     HIPCHK(c, hipGetLastError());
     if (c->timing) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
     int rc = check_status(c);
@@ -142,59 +142,45 @@ int compact(wcg_ctx* c) {
     return WCG_OK;
 }
 
-// LSD radix sort of recA[0:nrec) by the 128-bit prefix; result pointer in c->sorted
+// merge sort of recA[0:nrec) by the 128-bit prefix (no host round trip); result in c->sorted
 int sort_records(wcg_ctx* c) {
-    u64 n = c->nrec;
+    const u64 n = c->nrec;
     c->sorted = c->recA;
     if (n <= 1) return WCG_OK;
-    HIPCHK(c, hipMemsetAsync(c->st->hist, 0, sizeof(c->st->hist), c->stream));
-    k_hist16<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(c->recA, n, c->st);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(c->h_st->hist, c->st->hist, sizeof(c->st->hist), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    u32 nblocks = (u32)((n + RS_TILE - 1) / RS_TILE);
     Rec* src = c->recA;
     Rec* dst = c->recB;
-    for (int d = 0; d < 16; d++) {
-        bool trivial = false;
-        for (int x = 0; x < 256; x++)
-            if (c->h_st->hist[d][x] == n) { trivial = true; break; }
-        if (trivial) continue;
-        k_digit_hist<<<nblocks, RS_NT, 0, c->stream>>>(src, n, d, c->bh, nblocks);
-        k_scan_u32<<<1, 1024, 0, c->stream>>>(c->bh, (u64)nblocks * 256, nullptr);
-        k_scatter<<<nblocks, RS_NT, 0, c->stream>>>(src, dst, n, d, c->bh, nblocks);
+    k_tile_sort<<<(unsigned)((n + TS_TILE - 1) / TS_TILE), TS_NT, 0, c->stream>>>(src, dst, n);
+    HIPCHK(c, hipGetLastError());
+    std::swap(src, dst);
+    for (u64 w = TS_TILE; w < n; w *= 2) {
+        k_merge<<<(unsigned)((n + MG_CHUNK - 1) / MG_CHUNK), MG_NT, 0, c->stream>>>(src, dst, n, w);
         HIPCHK(c, hipGetLastError());
         std::swap(src, dst);
     }
     c->sorted = src;
-    // long keys sharing a 16-byte prefix
-    HIPCHK(c, hipMemsetAsync(&c->st->tie_flag, 0, sizeof(u32), c->stream));
-    k_tie_detect<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(c->sorted, n, c->st);
-    HIPCHK(c, hipMemcpyAsync(&c->h_st->tie_flag, &c->st->tie_flag, sizeof(u32), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->h_st->tie_flag) {
+    // long keys sharing a 16-byte prefix (needs two long keys at least)
+    if (c->h_st->nlong >= 2)
         k_tie_fix<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(c->sorted, n, c->arena);
-        HIPCHK(c, hipGetLastError());
-    }
+    HIPCHK(c, hipGetLastError());
     return WCG_OK;
 }
 
-// format sorted records; returns device buffer + size
+// format sorted records into a device buffer sized by an upper bound (so nothing waits for
+// the host before the write); one synchronisation at the end returns the exact size
 int format(wcg_ctx* c, int fmt, u32 nreduce, u32 part, uint8_t** dbuf, u64* cap, u64* nbytes) {
-    u64 n = c->nrec;
+    const u64 n = c->nrec;
     if (n == 0) { *nbytes = 0; return WCG_OK; }
-    int g = grid_for(n, 256, c->ncu * 8);
-    k_linelen<<<g, 256, 0, c->stream>>>(c->sorted, n, fmt, nreduce, part, c->arena, c->lens);
-    k_scan_u64<<<1, 1024, 0, c->stream>>>(c->lens, n, c->d_scalar);
-    HIPCHK(c, hipGetLastError());
-    u64 total = 0;
-    HIPCHK(c, hipMemcpyAsync(&total, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    int rc = ensure(c, dbuf, cap, total + 16);
+    const u64 bound = n * (15 + JSON_FIXED + 20) + c->h_st->arena_top + 64;
+    int rc = ensure(c, dbuf, cap, bound);
     if (rc) return rc;
-    k_write<<<g, 256, 0, c->stream>>>(c->sorted, n, fmt, nreduce, part, c->arena, c->lens, *dbuf);
+    const unsigned nt = (unsigned)((n + FM_TILE - 1) / FM_TILE);
+    k_fmt_sum<<<nt, FM_NT, 0, c->stream>>>(c->sorted, n, fmt, nreduce, part, c->arena, c->lens);
+    k_scan_u64<<<1, 1024, 0, c->stream>>>(c->lens, nt, c->d_scalar);
+    k_fmt_write<<<nt, FM_NT, 0, c->stream>>>(c->sorted, n, fmt, nreduce, part, c->arena, c->lens, *dbuf);
     HIPCHK(c, hipGetLastError());
-    *nbytes = total;
+    HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *nbytes = *c->h_scalar;
     return WCG_OK;
 }
 
@@ -242,10 +228,9 @@ int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx** 
     c->rec_cap = recs;
     HIPCHK(c, hipMalloc(&c->recA, recs * sizeof(Rec)));
     HIPCHK(c, hipMalloc(&c->recB, recs * sizeof(Rec)));
-    c->bh_cap = ((recs + RS_TILE - 1) / RS_TILE) * 256 + 256;
-    HIPCHK(c, hipMalloc(&c->bh, c->bh_cap * sizeof(u32)));
     HIPCHK(c, hipMalloc(&c->lens, recs * sizeof(u64)));
     HIPCHK(c, hipMalloc(&c->d_scalar, 64));
+    HIPCHK(c, hipHostMalloc(&c->h_scalar, 64, hipHostMallocDefault));
     HIPCHK(c, hipMalloc(&c->owner, recs * sizeof(u32)));
     HIPCHK(c, hipMalloc(&c->d_per_rank, 2 * 1024 * sizeof(u64)));
     return wcg_reset(c);
@@ -256,11 +241,12 @@ int wcg_close(wcg_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    void* bufs[] = {c->d_in, c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->bh, c->lens,
+    void* bufs[] = {c->d_in, c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens,
                     c->d_scalar, c->d_out, c->d_part, c->owner, c->d_per_rank, c->exp_buf,
                     c->pool, c->region_len};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
+    if (c->h_scalar) (void)hipHostFree(c->h_scalar);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return WCG_OK;
@@ -284,7 +270,7 @@ int wcg_reset(wcg_ctx* c) {
     if (rc) return rc;
     HIPCHK(c, hipMemsetAsync(c->gtab, 0, c->gslots * sizeof(GEntry), c->stream));
     HIPCHK(c, hipMemsetAsync(c->ltab, 0, c->lslots * sizeof(GEntry), c->stream));
-    HIPCHK(c, hipMemsetAsync(c->st, 0, offsetof(DevState, hist), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->st, 0, sizeof(DevState), c->stream));
     c->compacted = c->reduced = false;
     c->nrec = 0;
     c->out_len = 0;
@@ -313,13 +299,14 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     a.ltab = c->ltab; a.lmask = c->lslots - 1;
     a.arena = c->arena; a.arena_cap = c->arena_cap;
     a.st = c->st;
-    // miss log: one region per (workgroup, bucket); the whole pool is ~n bytes, enough for
-    // 0.4 entries per token of ordinary text; a full region falls back to the global table
+    // miss log: one region per (workgroup, bucket) of 8-byte units; the whole pool is ~n
+    // bytes, enough for ~0.7 misses per token of ordinary text; a full region falls back to
+    // the global table
     const u32 P = c->nbuckets;
     u64 per_wg_bytes = (u64)a.tiles_per_wg * MAP_STEP;
-    a.region_cap = std::max<u64>(1024, per_wg_bytes / (16ull * P));
+    a.region_cap = std::max<u64>(2048, per_wg_bytes / (8ull * P));
     a.pmask = P - 1;
-    u64 need = grid * P * a.region_cap * sizeof(uint4);
+    u64 need = grid * P * a.region_cap * sizeof(u64);
     if (need > c->pool_bytes) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (c->pool) HIPCHK(c, hipFree(c->pool));
@@ -507,7 +494,7 @@ int wcg_stats(wcg_ctx* c, uint64_t* s8) {
     if (!c || !s8) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, offsetof(DevState, hist), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     s8[0] = c->h_st->tokens; s8[1] = c->nrec; s8[2] = c->h_st->lds_hits; s8[3] = c->h_st->global_ops;
     s8[4] = c->h_st->long_tokens; s8[5] = c->h_st->arena_top; s8[6] = c->h_st->overflow; s8[7] = c->h_st->spin_fail;

@@ -63,11 +63,9 @@ struct DevState {
     u64 long_tokens;     // tokens longer than 15 bytes
     u64 arena_top;       // bytes used in the long-key arena
     u64 nrec;            // records produced by compaction
+    u64 nlong;           // ... of which long keys (> 15 bytes)
     u32 overflow;        // table / arena full -> WCG_EFULL
     u32 spin_fail;       // bounded spin gave up -> WCG_EFULL (never expected)
-    u32 tie_flag;        // two long keys share a 16-byte prefix
-    u32 pad;
-    u64 hist[16][256];   // global digit histograms for the sort
 };
 
 // ------------------------------------------------------------------ letters

@@ -1,12 +1,15 @@
 // wcg_lds_table.h - exact-key hash table in LDS (one per workgroup), 2-choice x 4-way buckets.
 //
-// Keys are the fixed-width inline identities of fact F4 (k0 = bytes 0-7, k1 = bytes 8-14 |
-// len << 56, never 0).  A key may occupy one of 8 slots: 4 in bucket b1 (hash bits 32-63) and
-// 4 in bucket b2 (bits 0-31).  Lookup reads the 4 first-words of a bucket with two
-// ds_read_b128; insertion claims an empty slot with a 64-bit LDS CAS on k0 and then publishes
-// k1.  Two lanes inserting the same new key at the same moment can end up in two different
-// slots: that duplicate is harmless (both counts are flushed and summed downstream), so no lane
-// ever waits for another lane's publish.
+// Keys are the fixed-width identities of fact F4 (k0 = bytes 0-7 [| len << 56 for len <= 7],
+// k1 = bytes 8-14 | len << 56 or 0).  A key may live in 8 slots: 4 in bucket b1 and 4 in
+// bucket b2.  A probe reads both buckets' k0 words (4 x ds_read_b128, independent), so a lookup
+// costs ONE LDS round trip; the measured alternatives (tag bytes first, or bucket b1 before b2)
+// add a dependent round trip and were slower.  The probe is split into start()
+// (issue the reads) and finish() (match / insert) so a lane can keep two lookups in flight.
+// Insertion claims an empty slot with a 64-bit LDS CAS on k0 and then publishes k1.  Two lanes
+// inserting the same new key at the same moment can end up in two different slots: that
+// duplicate is harmless (both counts are flushed and summed downstream), so no lane ever waits
+// for another lane's publish.
 #pragma once
 #include "wcg_common.h"
 
@@ -14,9 +17,14 @@ namespace wcg {
 
 template <int NB, typename CNT>
 struct LdsTable {
-    u64 (*k0)[4];
-    u64 (*k1)[4];
-    CNT (*cnt)[4];
+    u64 (*k0)[4];      // [NB][4]  (32-byte rows)
+    u64 (*k1)[4];      // [NB][4]
+    CNT (*cnt)[4];     // [NB][4]
+
+    struct Probe {
+        u32 b1, b2;
+        u64 v[4], w[4];
+    };
 
     __device__ __forceinline__ void init(int tid, int nt) {
         for (int i = tid; i < NB * 4; i += nt) {
@@ -32,32 +40,32 @@ struct LdsTable {
         if (b2 == b1) b2 = (b1 + 1 == (u32)NB) ? 0 : b1 + 1;
     }
 
-    __device__ __forceinline__ void add_cnt(u32 b, int j, CNT c) { atomicAdd(&cnt[b][j], c); }
-
     __device__ __forceinline__ void read4(u32 b, u64 (&v)[4]) const {
         const uint4* p = reinterpret_cast<const uint4*>(&k0[b][0]);
-        uint4 x = p[0], y = p[1];
+        const uint4 x = p[0], y = p[1];
         v[0] = (u64)x.y << 32 | x.x; v[1] = (u64)x.w << 32 | x.z;
         v[2] = (u64)y.y << 32 | y.x; v[3] = (u64)y.w << 32 | y.z;
     }
 
-    // aggregate (key, c) with h = lds_hash(key); false when both buckets hold other keys.
-    // Straight-line common path: both buckets are read, the 8 candidate slots become bit
-    // masks (slot s: bucket s >> 2, way s & 3), one LDS atomic at a computed address.
-    __device__ __forceinline__ bool add(u64 a0, u64 a1, u32 h, CNT c) {
-        u32 b1, b2;
-        buckets(h, b1, b2);
+    __device__ __forceinline__ void start(u32 h, Probe& p) const {
+        buckets(h, p.b1, p.b2);
+        read4(p.b1, p.v);
+        read4(p.b2, p.w);
+    }
+
+    __device__ __forceinline__ void add_cnt(u32 b, int j, CNT c) { atomicAdd(&cnt[b][j], c); }
+
+    // match (slot s: bucket s >> 2, way s & 3) or insert; false when both buckets are full of
+    // other keys.  Straight-line common path: bit masks and one atomic at a computed address.
+    __device__ __forceinline__ bool finish(u64 a0, u64 a1, const Probe& p, CNT c) {
         const bool shrt = key_short(a0);
-        u64 v[4], w[4];
-        read4(b1, v);
-        read4(b2, w);
         u32 m = 0, e = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            m |= (u32)(v[j] == a0) << j;
-            m |= (u32)(w[j] == a0) << (4 + j);
-            e |= (u32)(v[j] == 0) << j;
-            e |= (u32)(w[j] == 0) << (4 + j);
+            m |= (u32)(p.v[j] == a0) << j;
+            m |= (u32)(p.w[j] == a0) << (4 + j);
+            e |= (u32)(p.v[j] == 0) << j;
+            e |= (u32)(p.w[j] == 0) << (4 + j);
         }
         if (!shrt && m) {                       // keys of 8+ bytes: confirm k1 (usually 1 candidate)
             u32 mm = m;
@@ -65,18 +73,18 @@ struct LdsTable {
             while (mm) {
                 const int s = __ffs(mm) - 1;
                 mm &= mm - 1;
-                if (k1[s < 4 ? b1 : b2][s & 3] == a1) { m = 1u << s; break; }
+                if (k1[s < 4 ? p.b1 : p.b2][s & 3] == a1) { m = 1u << s; break; }
             }
         }
         if (m) {
             const int s = __ffs(m) - 1;
-            add_cnt(s < 4 ? b1 : b2, s & 3, c);
+            add_cnt(s < 4 ? p.b1 : p.b2, s & 3, c);
             return true;
         }
         while (e) {                             // insert: first empty slot of b1, then b2
             const int s = __ffs(e) - 1;
             e &= e - 1;
-            const u32 b = s < 4 ? b1 : b2;
+            const u32 b = s < 4 ? p.b1 : p.b2;
             const int j = s & 3;
             const u64 old = atomicCAS(&k0[b][j], 0ull, a0);
             if (old == 0) {
@@ -88,6 +96,12 @@ struct LdsTable {
         }
         return false;
     }
+
+    __device__ __forceinline__ bool add(u64 a0, u64 a1, u32 h, CNT c) {
+        Probe p;
+        start(h, p);
+        return finish(a0, a1, p, c);
+    }
 };
 
 // Hash-derived indices shared by every kernel that touches a key (they must agree):
@@ -98,8 +112,29 @@ struct LdsTable {
 __device__ __forceinline__ u32 miss_bucket(u64 h2, u32 pmask) { return (u32)h2 & pmask; }
 __device__ __forceinline__ u64 gslot(u64 h2) { return h2 >> 16; }
 
-// Miss-log entries are 16 bytes {k0, k1}.  A flushed LDS slot with count > 1 is written as
-// {k0, k1 | CNT_FLAG} followed by the carrier {0, count} (k0 == 0 marks a carrier / filler).
-constexpr u64 CNT_FLAG = 1ull << 63;
+// Miss-log units are 8 bytes; an entry is 1-3 units:
+//   short key (<= 7 bytes):   k0          (top byte = len, 1..7)
+//   medium key (8-15 bytes):  k0, k1      (k0 top byte = key byte 7, a letter byte >= 0x41;
+//                                          k1 top byte = len, 8..15)
+//   a count c > 1 sets U_CNT in the entry's last key unit and appends the unit c (top byte 0).
+// So every unit says what it is from its top byte T alone, and k_agg reads units in parallel:
+//   T == 0: count or filler (skip)     (T & 0x1F) < 8: short key      (T & 0x1F) >= 8, T < 0x41:
+//   medium-key tail (skip: owned by the head's reader)                 T >= 0x41: medium-key head
+constexpr u64 U_CNT = 1ull << 61;
+
+__device__ __forceinline__ int entry_units(u64 k0, u32 c) { return (key_short(k0) ? 1 : 2) + (c > 1 ? 1 : 0); }
+
+// write entry {k0, k1} x c at u[0..entry_units)
+__device__ __forceinline__ void put_entry(u64* u, u64 k0, u64 k1, u32 c) {
+    const u64 f = c > 1 ? U_CNT : 0;
+    if (key_short(k0)) {
+        u[0] = k0 | f;
+        if (c > 1) u[1] = c;
+    } else {
+        u[0] = k0;
+        u[1] = k1 | f;
+        if (c > 1) u[2] = c;
+    }
+}
 
 }  // namespace wcg

@@ -70,20 +70,23 @@ struct MapArgs {
     GEntry* ltab;  u64 lmask;      // long-key table
     uint8_t* arena; u64 arena_cap;
     DevState* st;
-    uint4* pool;   u64 region_cap;  // miss log: region (wg, p) = pool[(wg * P + p) * region_cap ...]
-    u32* region_len;               // entries written per region
+    u64* pool;     u64 region_cap;  // miss log: region (wg, p) = pool[(wg * P + p) * region_cap ...]
+    u32* region_len;               // units written per region
     u32 pmask;                     // P - 1 (P = number of miss buckets, power of two)
 };
 
-// append one miss-log entry for this workgroup; returns false when the region is full
-__device__ __forceinline__ bool log_push(const MapArgs& a, u32* cursor, u32 p, uint4 e) {
-    u32 pos = atomicAdd(&cursor[p], 1u);
-    if (pos >= a.region_cap) return false;
-    a.pool[((u64)blockIdx.x * (a.pmask + 1) + p) * a.region_cap + pos] = e;
-    return true;
-}
-__device__ __forceinline__ uint4 entry(u64 x, u64 y) {
-    return make_uint4((u32)x, (u32)(x >> 32), (u32)y, (u32)(y >> 32));
+// append one miss-log entry (wcg_lds_table.h) for this workgroup; false when the region is
+// full (the units of a region's last, cut-off entry are zeroed so k_agg skips them)
+__device__ __forceinline__ bool log_push(const MapArgs& a, u32* cursor, u32 p, u64 k0, u64 k1, u32 c) {
+    const u32 nu = (u32)entry_units(k0, c);
+    const u32 pos = atomicAdd(&cursor[p], nu);
+    u64* r = a.pool + ((u64)blockIdx.x * (a.pmask + 1) + p) * a.region_cap + pos;
+    if (pos + nu <= a.region_cap) {
+        put_entry(r, k0, k1, c);
+        return true;
+    }
+    for (u32 k = pos; k < a.region_cap; k++) r[k - pos] = 0;
+    return false;
 }
 
 __device__ __forceinline__ uint4 load_chunk(const uint8_t* in, u64 n, long pos) {
@@ -184,10 +187,12 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     // a uniform sample of it for its LDS table.
     const u64 nsteps = a.ntiles;
     const u64 stride = (u64)gridDim.x * MAP_WAVES;
-    // region chunk c <-> input bytes [step_base - PRE + 16c, +16): lane owns chunk lane+1,
-    // lane 0 also chunk 0 (prefix), lanes 1-4 also chunks 65-68 (look-ahead)
-    const int xc = (lane == 0) ? 0 : (lane <= 4 ? 64 + lane : -1);
-    u64 my_tokens = 0, my_hits = 0, my_global = 0, my_long = 0;
+    // region chunk c <-> input bytes [step_base - PRE + 16c, +16): lane owns chunk lane+1;
+    // lane 0 also chunk 0 (prefix), lane 63 chunk 65 (first look-ahead chunk, its DPP "next"),
+    // lanes 1-3 chunks 66-68 (rest of the 64-byte look-ahead used by the UTF-8 path)
+    const int xc = (lane == 0) ? 0 : (lane == 63 ? 65 : (lane <= 3 ? 65 + lane : -1));
+    u64 my_tokens = 0;                           // wave-uniform
+    u32 my_hits = 0, my_global = 0, my_long = 0;
 
     // Input loads: raw buffer loads through a per-step descriptor based at the step's prefix
     // (at the input start for step 0); the hardware range check returns zeros for the prefix
@@ -205,6 +210,15 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         const u32 ox = (live && xc >= 0) ? rel - MAP_PRE + 16 * xc : 0xFFFFFFF0u;
         m = buf_load16(rsrc, om);
         x = buf_load16(rsrc, ox);
+    };
+
+    // miss handling shared by both paths
+    auto miss = [&](u64 k0, u64 k1) {
+        const u64 h2 = key_hash(k0, k1);
+        if (!log_push(a, cursor, miss_bucket(h2, a.pmask), k0, k1, 1u)) {
+            my_global++;
+            ginsert(a.gtab, a.gmask, k0, k1, gslot(h2), 1, a.st);
+        }
     };
 
     auto process = [&](u64 step, const uint4 mine, const uint4 extra) {
@@ -262,22 +276,17 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        my_tokens += (lane == 0) ? (u64)total : 0;
+        my_tokens += total;
 
+        // ---- tokens, two per lane per iteration (i and i + 64): both tokens' LDS reads, then
+        //      both table probes, are issued before either result is used
         u32 sink = 0;
-        for (u32 i = lane; i < total; i += 64) {
-            if (ABL == 1) { sink += sst[i]; continue; }
-            const int off = sst[i];
+        auto token_key = [&](int off, int& len, u64& k0, u64& k1) {
             const int rp = MAP_PRE + off;                       // region position
             const int wi = rp >> 4, bi = rp & 15;
             const u32 w32 = (u32)msk[wi] | ((u32)msk[wi + 1] << 16);
             const u32 v = ~(w32 >> bi);                         // >= 17 valid bits
-            const int len = v ? __ffs(v) - 1 : 32;              // v == 0: run covers the window
-            if (len >= 16) {
-                my_long++;
-                long_token(a, (u64)(base + off));
-                continue;
-            }
+            len = v ? __ffs(v) - 1 : 32;                        // v == 0: run covers the window
             // key bytes [rp, rp+16) from LDS via 5 aligned dwords
             const int al = rp & ~3, sh = rp & 3;
             const u32* d = reinterpret_cast<const u32*>(bytes + al);
@@ -286,21 +295,33 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             const u32 o1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
             const u32 o2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
             const u32 o3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-            const u64 b0 = ((u64)o1 << 32 | o0) & low_bytes_mask(len);
-            const u64 b1 = len > 8 ? (((u64)o3 << 32 | o2) & low_bytes_mask(len - 8)) : 0ull;
-            u64 k0, k1;
-            make_key(b0, b1, len, k0, k1);
-            if (ABL == 2) { sink += lds_hash(k0, k1); continue; }
-            if (ABL == 3) { sink += tab.add(k0, k1, lds_hash(k0, k1), 1u); continue; }
-            if (tab.add(k0, k1, lds_hash(k0, k1), 1u)) {
-                my_hits++;
-            } else {
-                const u64 h2 = key_hash(k0, k1);
-                if (!log_push(a, cursor, miss_bucket(h2, a.pmask), entry(k0, k1))) {
-                    my_global++;
-                    ginsert(a.gtab, a.gmask, k0, k1, gslot(h2), 1, a.st);
-                }
-            }
+            const int kl = len < 16 ? len : 15;
+            const u64 b0 = ((u64)o1 << 32 | o0) & low_bytes_mask(kl);
+            const u64 b1 = kl > 8 ? (((u64)o3 << 32 | o2) & low_bytes_mask(kl - 8)) : 0ull;
+            make_key(b0, b1, kl, k0, k1);
+        };
+        for (u32 i = lane; i < total; i += 128) {
+            if (ABL == 1) { sink += sst[i] + (i + 64 < total ? sst[i + 64] : 0); continue; }
+            const bool vb = i + 64 < total;
+            const int offa = sst[i];
+            const int offb = vb ? sst[i + 64] : offa;
+            int la, lb;
+            u64 a0, a1, b0, b1;
+            token_key(offa, la, a0, a1);
+            token_key(offb, lb, b0, b1);
+            const bool sa = la < 16, sb = vb && lb < 16;        // inline keys (fact F4)
+            if (la >= 16) { my_long++; long_token(a, (u64)(base + offa)); }
+            if (vb && lb >= 16) { my_long++; long_token(a, (u64)(base + offb)); }
+            if (ABL == 2) { sink += lds_hash(a0, a1) + lds_hash(b0, b1); continue; }
+            typename decltype(tab)::Probe pa, pb;
+            if (sa) tab.start(lds_hash(a0, a1), pa);
+            if (sb) tab.start(lds_hash(b0, b1), pb);
+            const bool ha = sa && tab.finish(a0, a1, pa, 1u);
+            const bool hb = sb && tab.finish(b0, b1, pb, 1u);
+            if (ABL == 3) { sink += ha + hb; continue; }
+            my_hits += (u32)ha + (u32)hb;
+            if (sa && !ha) miss(a0, a1);
+            if (sb && !hb) miss(b0, b1);
         }
         if (ABL) asm volatile("" ::"v"(sink));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -308,56 +329,48 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
 
-    // two steps in flight per wave (A/B register sets, no copies between them); the step(s)
-    // reaching past the input end are reloaded byte-exactly (cold, separate call site)
+    // two steps in flight per wave (A/B register sets, no copies between them).  A wave's
+    // steps increase, so once one reaches past the input end (a "tail" step) all later ones do:
+    // the main loop stops there and the tail steps are reloaded byte-exactly after it (keeping
+    // the cold reload path's registers out of the loop)
     auto is_tail = [&](u64 step) { return step * MAP_STEP + MAP_STEP + MAP_LOOK > a.n; };
-    auto tail_chunk = [&](u64 step, int c) -> uint4 {
-        return load_chunk(a.in, a.n, (long)(step * MAP_STEP) - MAP_PRE + 16 * c);
-    };
     auto u4 = [](v4u v) { return make_uint4(v.x, v.y, v.z, v.w); };
     v4u ma, xa, mb, xb;
     u64 st = (u64)blockIdx.x * MAP_WAVES + wave;
     load(st, ma, xa);
     load(st + stride, mb, xb);
-    for (; st < nsteps; st += 2 * stride) {
+    while (st < nsteps && !is_tail(st)) {
         buf_wait<2>(ma, xa);                     // younger: B's two loads
-        if (is_tail(st)) process(st, tail_chunk(st, lane + 1), xc >= 0 ? tail_chunk(st, xc) : u4(xa));
-        else process(st, u4(ma), u4(xa));
+        process(st, u4(ma), u4(xa));
         load(st + 2 * stride, ma, xa);
+        st += stride;
+        if (st >= nsteps || is_tail(st)) break;
         buf_wait<2>(mb, xb);                     // younger: A's two loads
-        const u64 sb = st + stride;
-        if (sb >= nsteps) break;
-        if (is_tail(sb)) process(sb, tail_chunk(sb, lane + 1), xc >= 0 ? tail_chunk(sb, xc) : u4(xb));
-        else process(sb, u4(mb), u4(xb));
-        load(st + 3 * stride, mb, xb);
+        process(st, u4(mb), u4(xb));
+        load(st + 2 * stride, mb, xb);
+        st += stride;
     }
     buf_wait<0>(ma, xa);                         // nothing may land in a dead register
     buf_wait<0>(mb, xb);
+    for (; st < nsteps; st += stride) {
+        const long org = (long)(st * MAP_STEP) - MAP_PRE;
+        const uint4 mine = load_chunk(a.in, a.n, org + 16 * (lane + 1));
+        const uint4 extra = xc >= 0 ? load_chunk(a.in, a.n, org + 16 * xc) : make_uint4(0, 0, 0, 0);
+        process(st, mine, extra);
+    }
 
-    // ---- flush the LDS table into this workgroup's miss-log regions (count 1: one entry,
-    //      count c > 1: {k0, k1|CNT_FLAG} + carrier {0, c}); a full region -> global table
+    // ---- flush the LDS table into this workgroup's miss-log regions (entries with counts);
+    //      a full region -> global table
     __syncthreads();
     for (int i = tid; i < MAP_NB * 4; i += MAP_NT) {
         const u32 c = (&tcnt[0][0])[i];
         if (!c) continue;
         const u64 k0 = (&tk0[0][0])[i], k1 = (&tk1[0][0])[i];
         const u64 h2 = key_hash(k0, k1);
-        const u32 p = miss_bucket(h2, a.pmask);
-        bool ok;
-        if (c == 1) {
-            ok = log_push(a, cursor, p, entry(k0, k1));
-        } else {
-            const u32 pos = atomicAdd(&cursor[p], 2u);
-            uint4* r = a.pool + ((u64)blockIdx.x * (a.pmask + 1) + p) * a.region_cap + pos;
-            ok = pos + 1 < a.region_cap;
-            if (ok) {
-                r[0] = entry(k0, k1 | CNT_FLAG);
-                r[1] = entry(0, (u64)c);
-            } else if (pos < a.region_cap) {
-                r[0] = entry(0, 0);                 // last slot of the region: a filler k_agg skips
-            }
+        if (!log_push(a, cursor, miss_bucket(h2, a.pmask), k0, k1, c)) {
+            my_global++;
+            ginsert(a.gtab, a.gmask, k0, k1, gslot(h2), c, a.st);
         }
-        if (!ok) { my_global++; ginsert(a.gtab, a.gmask, k0, k1, gslot(h2), c, a.st); }
     }
     __syncthreads();
     for (u32 p = tid; p <= a.pmask; p += MAP_NT) {
@@ -365,7 +378,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         a.region_len[(u64)blockIdx.x * (a.pmask + 1) + p] = c < a.region_cap ? c : (u32)a.region_cap;
     }
     // stats: one atomic per wave
-    u64 v0 = my_tokens, v1 = my_hits, v2 = my_global, v3 = my_long;
+    u64 v0 = lane == 0 ? my_tokens : 0, v1 = my_hits, v2 = my_global, v3 = my_long;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         v0 += __shfl_xor(v0, d, 64); v1 += __shfl_xor(v1, d, 64);

@@ -1,12 +1,10 @@
 // wcg_reduce.h - DoReduce + Merge on gfx950 (mapreduce.go:239-321, wc.go:35-38).
 //
 //   k_compact   global tables -> dense records {128-bit big-endian prefix, count, ref}
-//   k_hist16    one pass over the records: global histogram of all 16 prefix bytes, so the
-//               host can skip sort passes whose digit is constant (fact F4 makes the
+//   k_tile_sort / k_merge   merge sort by the 128-bit big-endian prefix (fact F4 makes the
 //               zero-padded prefix Go's sort.Strings order for keys <= 15 bytes)
-//   k_digit_hist / k_scan / k_scatter   one stable LSD radix pass over an 8-bit digit
-//   k_ties      long keys (> 15 bytes) that share a 16-byte prefix: ordered by full bytes
-//   k_linelen / k_scan / k_write        "key: count\n" (Merge, mapreduce.go:316-318) or
+//   k_tie_fix   long keys (> 15 bytes) that share a 16-byte prefix: ordered by full bytes
+//   k_fmt_sum / k_scan_u64 / k_fmt_write  "key: count\n" (Merge, mapreduce.go:316-318) or
 //               {"Key":"k","Value":"count"}\n for ihash(k)%R == r (DoReduce, :274-278)
 #pragma once
 #include "wcg_common.h"
@@ -14,122 +12,199 @@
 
 namespace wcg {
 
-constexpr int RS_NT = 256;            // threads per sort block
-constexpr int RS_IPT = 8;             // records per thread
-constexpr int RS_TILE = RS_NT * RS_IPT;
-
 // ---------------------------------------------------------------- compaction
-__global__ void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots, const uint8_t* arena,
-                          Rec* out, DevState* st) {
+constexpr int CP_NT = 256, CP_IPT = 8;          // 2048 table slots per block, one atomic each
+
+__device__ __forceinline__ bool slot_to_rec(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 total, u64 i,
+                                            const uint8_t* arena, Rec& r) {
+    if (i < gslots) {
+        const GEntry e = gtab[i];
+        if (e.k0 == 0) return false;
+        if (key_short(e.k0)) {
+            r.hi = bswap64(e.k0 & 0x00FFFFFFFFFFFFFFull);
+            r.lo = 0;
+            r.ref = e.k0 >> 56;
+        } else {
+            r.hi = bswap64(e.k0);
+            r.lo = bswap64(e.k1 & 0x00FFFFFFFFFFFFFFull);
+            r.ref = e.k1 >> 56;
+        }
+        r.cnt = e.cnt;
+        return true;
+    }
+    if (i >= total) return false;
+    const GEntry e = ltab[i - gslots];
+    if (e.k0 == 0) return false;
+    const u64 off = e.k1 - 1, len = e.aux;
+    u64 hi = 0, lo = 0;
+    for (int k = 0; k < 8; k++) hi = (hi << 8) | arena[off + k];
+    for (int k = 8; k < 16; k++) lo = (lo << 8) | arena[off + k];
+    r.hi = hi; r.lo = lo; r.cnt = e.cnt;
+    r.ref = LONG_FLAG | (len << 40) | off;
+    return true;
+}
+
+__global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
+                                                  const uint8_t* arena, Rec* out, DevState* st) {
+    __shared__ u32 wsum[CP_NT / 64];
+    __shared__ u64 base_s;
     const u64 total = gslots + lslots;
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i - threadIdx.x < total; i += (u64)gridDim.x * blockDim.x) {
-        Rec r;
-        bool have = false;
-        if (i < gslots) {
-            GEntry e = gtab[i];
-            if (e.k0 != 0) {
-                have = true;
-                if (key_short(e.k0)) {
-                    r.hi = bswap64(e.k0 & 0x00FFFFFFFFFFFFFFull);
-                    r.lo = 0;
-                    r.ref = e.k0 >> 56;
-                } else {
-                    r.hi = bswap64(e.k0);
-                    r.lo = bswap64(e.k1 & 0x00FFFFFFFFFFFFFFull);
-                    r.ref = e.k1 >> 56;
-                }
-                r.cnt = e.cnt;
-            }
-        } else if (i < total) {
-            GEntry e = ltab[i - gslots];
-            if (e.k0 != 0) {
-                have = true;
-                u64 off = e.k1 - 1, len = e.aux;
-                u64 hi = 0, lo = 0;
-                for (int k = 0; k < 8; k++) hi = (hi << 8) | arena[off + k];
-                for (int k = 8; k < 16; k++) lo = (lo << 8) | arena[off + k];
-                r.hi = hi; r.lo = lo; r.cnt = e.cnt;
-                r.ref = LONG_FLAG | (len << 40) | off;
-            }
-        }
-        u64 bal = __ballot(have);
-        if (bal == 0) continue;
-        const int lane = threadIdx.x & 63;
-        u64 base = 0;
-        int leader = __ffsll((long long)bal) - 1;
-        if (lane == leader) base = atomicAdd(&st->nrec, (u64)__popcll(bal));
-        base = __shfl(base, leader, 64);
-        if (have) out[base + __popcll(bal & ((1ull << lane) - 1))] = r;
-    }
-}
-
-__device__ __forceinline__ u32 rec_digit(const Rec& r, int d) {
-    return d < 8 ? (u32)(r.lo >> (8 * d)) & 0xFF : (u32)(r.hi >> (8 * (d - 8))) & 0xFF;
-}
-
-__global__ void k_hist16(const Rec* recs, u64 n, DevState* st) {
-    __shared__ u32 h[16][256];
-    for (int i = threadIdx.x; i < 16 * 256; i += blockDim.x) (&h[0][0])[i] = 0;
-    __syncthreads();
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        Rec r = recs[i];
-#pragma unroll
-        for (int d = 0; d < 16; d++) atomicAdd(&h[d][rec_digit(r, d)], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 16 * 256; i += blockDim.x) {
-        u32 v = (&h[0][0])[i];
-        if (v) atomicAdd(&(&st->hist[0][0])[i], (u64)v);
-    }
-}
-
-// per-block digit histogram, digit-major: bh[d * nblocks + b]
-__global__ __launch_bounds__(RS_NT) void k_digit_hist(const Rec* recs, u64 n, int d, u32* bh, u32 nblocks) {
-    __shared__ u32 h[256];
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const u64 b0 = (u64)blockIdx.x * RS_TILE;
-    for (int j = 0; j < RS_IPT; j++) {
-        u64 i = b0 + (u64)j * RS_NT + threadIdx.x;
-        if (i < n) atomicAdd(&h[rec_digit(recs[i], d)], 1u);
-    }
-    __syncthreads();
-    bh[(u64)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
-}
-
-// exclusive scan of u32 (in place) by one workgroup of 1024 threads; returns total in *total
-__global__ __launch_bounds__(1024) void k_scan_u32(u32* v, u64 n, u64* total) {
-    __shared__ u32 ws[16];
-    __shared__ u32 carry_s;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) carry_s = 0;
-    __syncthreads();
-    for (u64 base = 0; base < n; base += 1024 * 4) {
-        u32 x[4], s = 0;
-        for (int k = 0; k < 4; k++) {
-            u64 i = base + (u64)tid * 4 + k;
-            x[k] = i < n ? v[i] : 0;
-            s += x[k];
+    const u64 b0 = (u64)blockIdx.x * CP_NT * CP_IPT;
+    Rec r[CP_IPT];
+    u32 have = 0, nlong = 0;
+#pragma unroll
+    for (int j = 0; j < CP_IPT; j++)
+        if (slot_to_rec(gtab, gslots, ltab, total, b0 + (u64)j * CP_NT + tid, arena, r[j])) {
+            have |= 1u << j;
+            nlong += (r[j].ref & LONG_FLAG) ? 1 : 0;
         }
-        u32 incl = s;
-        for (int d = 1; d < 64; d <<= 1) { u32 y = __shfl_up(incl, d, 64); if (lane >= d) incl += y; }
-        if (lane == 63) ws[w] = incl;
-        __syncthreads();
-        u32 wpre = 0, all = 0;
-        for (int k = 0; k < 16; k++) { if (k < w) wpre += ws[k]; all += ws[k]; }
-        u32 run = carry_s + wpre + incl - s;
-        for (int k = 0; k < 4; k++) {
-            u64 i = base + (u64)tid * 4 + k;
-            if (i < n) v[i] = run;
-            run += x[k];
-        }
-        __syncthreads();
-        if (tid == 0) carry_s += all;
-        __syncthreads();
+    if (nlong) atomicAdd(&st->nlong, (u64)nlong);
+    const u32 cnt = __popc(have);
+    // block exclusive prefix of cnt (<= 8 per thread): 4 ballots per wave, then waves in order
+    u32 o = 0, wt = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const u64 bal = __ballot((cnt >> b) & 1);
+        o += __builtin_amdgcn_mbcnt_hi((u32)(bal >> 32), __builtin_amdgcn_mbcnt_lo((u32)bal, 0u)) << b;
+        wt += (u32)__popcll(bal) << b;
     }
-    if (tid == 0 && total) *total = carry_s;
+    if (lane == 0) wsum[w] = wt;
+    __syncthreads();
+    if (tid == 0) {
+        u32 all = 0;
+        for (int k = 0; k < CP_NT / 64; k++) { const u32 v = wsum[k]; wsum[k] = all; all += v; }
+        base_s = all ? atomicAdd(&st->nrec, (u64)all) : 0;
+    }
+    __syncthreads();
+    u64 pos = base_s + wsum[w] + o;
+#pragma unroll
+    for (int j = 0; j < CP_IPT; j++)
+        if (have & (1u << j)) out[pos++] = r[j];
 }
 
+// ---------------------------------------------------------------- sort
+// Merge sort on the 128-bit big-endian prefix: k_tile_sort orders each 2048-record tile with an
+// LDS bitonic network, then log2(n / 2048) k_merge passes double the sorted run length.  Cost
+// does not depend on the key distribution (a radix sort's MSD buckets collapse on UTF-8 text,
+// where every word of a script shares its first byte or two) and no pass needs the host.
+constexpr int TS_NT = 1024, TS_TILE = 2048;
+constexpr int MG_NT = 256, MG_CHUNK = 1024;
+
+__device__ __forceinline__ bool pre_lt(u64 ah, u64 al, u64 bh, u64 bl) { return ah < bh || (ah == bh && al < bl); }
+
+__global__ __launch_bounds__(TS_NT) void k_tile_sort(const Rec* in, Rec* out, u64 n) {
+    __shared__ u64 sh[TS_TILE], sl[TS_TILE];
+    __shared__ uint16_t si[TS_TILE];
+    const u64 base = (u64)blockIdx.x * TS_TILE;
+    const int tid = threadIdx.x;
+    for (int k = 0; k < TS_TILE / TS_NT; k++) {
+        const int i = k * TS_NT + tid;
+        const u64 g = base + i;
+        if (g < n) {
+            const Rec r = in[g];
+            sh[i] = r.hi; sl[i] = r.lo;
+        } else {                                  // padding: no key has an all-0xFF prefix
+            sh[i] = ~0ull; sl[i] = ~0ull;
+        }
+        si[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    for (int k = 2; k <= TS_TILE; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int q = 0; q < TS_TILE / 2 / TS_NT; q++) {
+                const int t = q * TS_NT + tid;               // compare-exchange pair t
+                const int i = 2 * t - (t & (j - 1)), p = i + j;
+                const u64 ah = sh[i], al = sl[i], bh = sh[p], bl = sl[p];
+                if (pre_lt(bh, bl, ah, al) == ((i & k) == 0)) {
+                    sh[i] = bh; sl[i] = bl; sh[p] = ah; sl[p] = al;
+                    const uint16_t x = si[i]; si[i] = si[p]; si[p] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int k = 0; k < TS_TILE / TS_NT; k++) {
+        const int i = k * TS_NT + tid;
+        if (base + i < n) out[base + i] = in[base + si[i]];
+    }
+}
+
+// merge path: number of A records among the first d outputs of merge(A, B) (A first on equal
+// prefixes).  One wave, 64-way search: each round samples 64 split candidates, so a run of a
+// million records is settled in four rounds of two loads each.
+__device__ __forceinline__ u64 merge_split(const Rec* A, u64 la, const Rec* B, u64 lb, u64 d, int lane) {
+    u64 lo = d > lb ? d - lb : 0, hi = d < la ? d : la;
+    while (hi > lo) {
+        const u64 s = hi - lo;
+        const u64 p = s <= 64 ? lo + lane : lo + (u64)lane * s / 64;
+        bool t = false;
+        if (p < hi) {
+            const Rec& x = A[p];
+            const Rec& y = B[d - 1 - p];
+            t = !pre_lt(y.hi, y.lo, x.hi, x.lo);
+        }
+        const int c = __popcll(__ballot(t));
+        if (s <= 64) return lo + c;
+        const u64 nlo = c > 0 ? __shfl(p, c - 1) + 1 : lo;
+        const u64 nhi = c < 64 ? __shfl(p, c) : hi;
+        lo = nlo; hi = nhi;
+    }
+    return lo;
+}
+
+// one merge pass: runs of length w -> 2w; workgroup b writes outputs [b * 1024, +1024)
+__global__ __launch_bounds__(MG_NT) void k_merge(const Rec* in, Rec* out, u64 n, u64 w) {
+    __shared__ u64 sh[MG_CHUNK], sl[MG_CHUNK];
+    __shared__ u64 split[2];
+    const u64 c0 = (u64)blockIdx.x * MG_CHUNK;
+    const u64 a0 = c0 / (2 * w) * (2 * w);
+    const u64 la = n - a0 < w ? n - a0 : w;
+    const u64 rest = n - a0 - la;
+    const u64 lb = rest < w ? rest : w;
+    const Rec* A = in + a0;
+    const Rec* B = A + la;
+    const u64 d0 = c0 - a0, d1 = (d0 + MG_CHUNK < la + lb) ? d0 + MG_CHUNK : la + lb;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (wv < 2) {
+        const u64 sp = merge_split(A, la, B, lb, wv ? d1 : d0, lane);
+        if (lane == 0) split[wv] = sp;
+    }
+    __syncthreads();
+    const u64 i0 = split[0], i1 = split[1];
+    const u64 j0 = d0 - i0;
+    const int na = (int)(i1 - i0), m = (int)(d1 - d0);
+    Rec r[MG_CHUNK / MG_NT];
+#pragma unroll
+    for (int k = 0; k < MG_CHUNK / MG_NT; k++) {
+        const int e = k * MG_NT + tid;
+        if (e < m) {
+            r[k] = e < na ? A[i0 + e] : B[j0 + (e - na)];
+            sh[e] = r[k].hi; sl[e] = r[k].lo;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MG_CHUNK / MG_NT; k++) {
+        const int e = k * MG_NT + tid;
+        if (e >= m) continue;
+        const u64 xh = r[k].hi, xl = r[k].lo;
+        int lo, hi, pos;
+        if (e < na) {                              // B window records strictly below x
+            lo = na; hi = m;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (pre_lt(sh[mid], sl[mid], xh, xl)) lo = mid + 1; else hi = mid; }
+            pos = e + (lo - na);
+        } else {                                   // A window records at or below x
+            lo = 0; hi = na;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (!pre_lt(xh, xl, sh[mid], sl[mid])) lo = mid + 1; else hi = mid; }
+            pos = (e - na) + lo;
+        }
+        out[a0 + d0 + pos] = r[k];
+    }
+}
+
+// exclusive scan of u64 (in place) by one workgroup of 1024 threads; total in *total
 __global__ __launch_bounds__(1024) void k_scan_u64(u64* v, u64 n, u64* total) {
     __shared__ u64 ws[16];
     __shared__ u64 carry_s;
@@ -162,43 +237,6 @@ __global__ __launch_bounds__(1024) void k_scan_u64(u64* v, u64 n, u64* total) {
     if (tid == 0 && total) *total = carry_s;
 }
 
-// stable scatter for digit d; records of a block are ranked in index order
-__global__ __launch_bounds__(RS_NT) void k_scatter(const Rec* in, Rec* out, u64 n, int d, const u32* boff, u32 nblocks) {
-    __shared__ u32 run[256];          // block-local count of each digit so far
-    __shared__ u32 wh[RS_NT / 64][256];
-    __shared__ u32 goff[256];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    run[tid] = 0;
-    goff[tid] = boff[(u64)tid * nblocks + blockIdx.x];
-    const u64 b0 = (u64)blockIdx.x * RS_TILE;
-    for (int j = 0; j < RS_IPT; j++) {
-        for (int k = 0; k < RS_NT / 64; k++) wh[k][tid] = 0;
-        __syncthreads();
-        u64 i = b0 + (u64)j * RS_NT + tid;
-        bool valid = i < n;
-        Rec r;
-        u32 dg = 0;
-        if (valid) { r = in[i]; dg = rec_digit(r, d); }
-        // lanes of this wave holding the same digit
-        u64 peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-            u64 bb = __ballot((dg >> b) & 1);
-            peers &= ((dg >> b) & 1) ? bb : ~bb;
-        }
-        u32 rank_in_wave = (u32)__popcll(peers & ((1ull << lane) - 1));
-        if (valid && rank_in_wave == 0) wh[w][dg] = (u32)__popcll(peers);
-        __syncthreads();
-        // digit tid: offsets of each wave = run + counts of earlier waves
-        u32 acc = run[tid];
-        for (int k = 0; k < RS_NT / 64; k++) { u32 c = wh[k][tid]; wh[k][tid] = acc; acc += c; }
-        run[tid] = acc;
-        __syncthreads();
-        if (valid) out[goff[dg] + wh[w][dg] + rank_in_wave] = r;
-        __syncthreads();
-    }
-}
-
 // ---------------------------------------------------------------- long-key ties
 __device__ int cmp_full(const Rec& a, const Rec& b, const uint8_t* arena) {
     // both long: compare full bytes
@@ -208,11 +246,6 @@ __device__ int cmp_full(const Rec& a, const Rec& b, const uint8_t* arena) {
     u64 m = la < lb ? la : lb;
     for (u64 i = 0; i < m; i++) if (pa[i] != pb[i]) return pa[i] < pb[i] ? -1 : 1;
     return la < lb ? -1 : (la > lb ? 1 : 0);
-}
-
-__global__ void k_tie_detect(const Rec* r, u64 n, DevState* st) {
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i + 1 < n; i += (u64)gridDim.x * blockDim.x)
-        if (r[i].hi == r[i + 1].hi && r[i].lo == r[i + 1].lo) atomicOr(&st->tie_flag, 1u);
 }
 
 // one thread per run of equal prefixes: insertion sort by full key bytes
@@ -253,23 +286,55 @@ __device__ u32 rec_ihash(const Rec& r, const uint8_t* arena) {
 constexpr int FMT_MERGED = 0, FMT_JSON = 1;
 constexpr u64 JSON_FIXED = 8 + 11 + 3;   // {"Key":" + ","Value":" + "}\n
 
-__global__ void k_linelen(const Rec* r, u64 n, int fmt, u32 nreduce, u32 part, const uint8_t* arena, u64* len) {
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        Rec x = r[i];
-        u64 L;
-        if (fmt == FMT_MERGED) L = rec_len(x) + 3 + ndigits(x.cnt);
-        else L = (rec_ihash(x, arena) % nreduce == part) ? rec_len(x) + JSON_FIXED + ndigits(x.cnt) : 0;
-        len[i] = L;
-    }
+__device__ __forceinline__ u64 line_len(const Rec& x, int fmt, u32 nreduce, u32 part, const uint8_t* arena) {
+    if (fmt == FMT_MERGED) return rec_len(x) + 3 + ndigits(x.cnt);
+    return (rec_ihash(x, arena) % nreduce == part) ? rec_len(x) + JSON_FIXED + ndigits(x.cnt) : 0;
 }
 
-__global__ void k_write(const Rec* r, u64 n, int fmt, u32 nreduce, u32 part, const uint8_t* arena, const u64* off,
-                        uint8_t* out) {
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        Rec x = r[i];
-        if (fmt == FMT_JSON && rec_ihash(x, arena) % nreduce != part) continue;
-        uint8_t* o = out + off[i];
-        u64 len = rec_len(x);
+// Formatting runs in tiles of 1024 lines (4 consecutive lines per thread): k_fmt_sum writes each
+// tile's byte count, k_scan_u64 turns those into tile offsets, k_fmt_write recomputes its lines'
+// lengths, scans them inside the tile and writes the bytes.
+constexpr int FM_NT = 256, FM_IPT = 4, FM_TILE = FM_NT * FM_IPT;
+
+__device__ __forceinline__ u64 block_excl_scan(u64 s, u64* ws, u64& all) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    u64 incl = s;
+    for (int d = 1; d < 64; d <<= 1) { const u64 y = __shfl_up(incl, d, 64); if (lane >= d) incl += y; }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    u64 pre = 0;
+    all = 0;
+    for (int k = 0; k < FM_NT / 64; k++) { if (k < w) pre += ws[k]; all += ws[k]; }
+    return pre + incl - s;
+}
+
+__global__ __launch_bounds__(FM_NT) void k_fmt_sum(const Rec* r, u64 n, int fmt, u32 nreduce, u32 part,
+                                                  const uint8_t* arena, u64* tsum) {
+    __shared__ u64 ws[FM_NT / 64];
+    const u64 i0 = (u64)blockIdx.x * FM_TILE + (u64)threadIdx.x * FM_IPT;
+    u64 s = 0;
+    for (int k = 0; k < FM_IPT; k++)
+        if (i0 + k < n) s += line_len(r[i0 + k], fmt, nreduce, part, arena);
+    u64 all;
+    (void)block_excl_scan(s, ws, all);
+    if (threadIdx.x == 0) tsum[blockIdx.x] = all;
+}
+
+__global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, int fmt, u32 nreduce, u32 part,
+                                                    const uint8_t* arena, const u64* toff, uint8_t* out) {
+    __shared__ u64 ws[FM_NT / 64];
+    const u64 i0 = (u64)blockIdx.x * FM_TILE + (u64)threadIdx.x * FM_IPT;
+    u64 L[FM_IPT], s = 0;
+    for (int k = 0; k < FM_IPT; k++) {
+        L[k] = i0 + k < n ? line_len(r[i0 + k], fmt, nreduce, part, arena) : 0;
+        s += L[k];
+    }
+    u64 all;
+    uint8_t* o = out + toff[blockIdx.x] + block_excl_scan(s, ws, all);
+    for (int q = 0; q < FM_IPT; q++) {
+        if (L[q] == 0) continue;
+        const Rec x = r[i0 + q];
+        const u64 len = rec_len(x);
         if (fmt == FMT_JSON) {
             const char* pre = "{\"Key\":\"";
             for (int k = 0; k < 8; k++) *o++ = pre[k];
@@ -281,12 +346,12 @@ __global__ void k_write(const Rec* r, u64 n, int fmt, u32 nreduce, u32 part, con
         } else {
             *o++ = ':'; *o++ = ' ';
         }
-        u32 nd = ndigits(x.cnt);
+        const u32 nd = ndigits(x.cnt);
         u64 c = x.cnt;
         for (int k = (int)nd - 1; k >= 0; k--) { o[k] = (uint8_t)('0' + c % 10); c /= 10; }
         o += nd;
         if (fmt == FMT_JSON) { *o++ = '"'; *o++ = '}'; }
-        *o = '\n';
+        *o++ = '\n';
     }
 }
 
