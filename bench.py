@@ -152,6 +152,9 @@ def main():
             got = eng.result()
             data = host.numpy().tobytes()
             verified = got == ob.merged(data, 16)
+            if not verified:
+                sys.stderr.write("bench: GPU result differs from the oracle; refusing to report a rate\n")
+                sys.exit(3)
         else:
             # every rank sends its input size; root checks token totals via the oracle on its own range
             verified = None

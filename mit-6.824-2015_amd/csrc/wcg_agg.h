@@ -13,8 +13,9 @@
 namespace wcg {
 
 constexpr int AGG_NT = 1024;
-constexpr int AGG_ILP = 4;
+constexpr u32 AGG_BATCH = AGG_NT * 4;     // units per batch (4 per thread)
 constexpr int AGG_NB = 1696;           // 1696 x 4 slots x 24 B (u64 counts) = 162816 B
+constexpr u32 AGG_MAX_SRC = 256;       // source regions per workgroup (+1 KiB LDS = 160 KiB)
 
 struct AggArgs {
     const u64* pool;
@@ -32,64 +33,88 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     __shared__ __align__(16) u64 tk0[AGG_NB][4];
     __shared__ __align__(16) u64 tk1[AGG_NB][4];
     __shared__ u64 tcnt[AGG_NB][4];
+    __shared__ u32 rlen_s[AGG_MAX_SRC];
     const int tid = threadIdx.x;
     LdsTable<AGG_NB, u64> tab{tk0, tk1, tcnt};
     tab.init(tid, AGG_NT);
-    __syncthreads();
-
     const u32 p = blockIdx.x % a.P, s = blockIdx.x / a.P;
     const u32 w0 = (u32)(((u64)a.nsrc * s) / a.slices), w1 = (u32)(((u64)a.nsrc * (s + 1)) / a.slices);
+    // region lengths of this slice, staged once: a global load in the batch walk would be a
+    // vmcnt wait that drains the prefetch
+    for (u32 w = w0 + tid; w < w1; w += AGG_NT) rlen_s[w - w0] = a.region_len[(u64)w * a.P + p];
+    __syncthreads();
     u64 my_global = 0;
-    // units are read AGG_ILP at a time per thread (independent loads in flight), decoded, and
-    // looked up two at a time (both probes' bucket reads issued before either is matched)
-    auto decode = [&](const u64* base, u32 i, u64 u, u64& k0, u64& k1, u64& c) -> bool {
-        const u32 T = (u32)(u >> 56);
-        if (T == 0) return false;                            // count / filler
-        bool has;
-        u32 j;
-        k1 = 0;
-        if (T < 0x41) {
-            if ((T & 0x1F) >= 8) return false;               // medium-key tail
-            k0 = u & ~U_CNT;
-            has = (u & U_CNT) != 0;
-            j = i + 1;
-        } else {
-            k0 = u;
-            k1 = base[i + 1];
-            has = (k1 & U_CNT) != 0;
-            k1 &= ~U_CNT;
-            j = i + 2;
-        }
-        c = has ? base[j] : 1;
-        return true;
+    // Batches: thread t of a batch takes units [4t, 4t + 4) of one region and also loads the
+    // two after them, so a medium-key head or a count flag finds its neighbours in registers
+    // (units past the region's length are masked to 0 = filler).  The next batch is loaded into
+    // the other register set while this one is aggregated.  (Compiler-managed loads: the
+    // hand-counted asm loads of k_map measured no faster here.)
+    auto rlen = [&](u32 w) -> u32 { return rlen_s[w - w0]; };
+    auto next_batch = [&](u32& w, u32& b) {          // wave-uniform walk over non-empty batches
+        b++;
+        while (w < w1 && (u64)b * AGG_BATCH >= rlen(w)) { w++; b = 0; }
     };
-    auto spill = [&](u64 k0, u64 k1, u64 c) {
-        my_global++;
-        ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
+    auto load = [&](u32 w, u32 b, v4u& x0, v4u& x1, v4u& x2) {
+        const bool live = w < w1;
+        const u32 i = b * AGG_BATCH + 4 * tid, lim = live ? rlen(w) : 0;
+        const v4u* q = reinterpret_cast<const v4u*>(a.pool + ((u64)(live ? w : w0) * a.P + p) * a.region_cap + i);
+        const v4u z = {0, 0, 0, 0};
+        x0 = i < lim ? q[0] : z;
+        x1 = i + 2 < lim ? q[1] : z;
+        x2 = i + 4 < lim ? q[2] : z;
     };
-    for (u32 w = w0; w < w1; w++) {
-        const u64 reg = (u64)w * a.P + p;
-        const u32 len = a.region_len[reg];
-        const u64* base = a.pool + reg * a.region_cap;
-        for (u32 i0 = tid; i0 < len; i0 += AGG_NT * AGG_ILP) {
-            u64 u[AGG_ILP];
+    auto unit = [](const v4u& x, int h) -> u64 { return h ? ((u64)x.w << 32 | x.z) : ((u64)x.y << 32 | x.x); };
+    auto process = [&](u32 w, u32 b, const v4u& x0, const v4u& x1, const v4u& x2) {
+        u64 u[6] = {unit(x0, 0), unit(x0, 1), unit(x1, 0), unit(x1, 1), unit(x2, 0), unit(x2, 1)};
+        const u32 i0 = b * AGG_BATCH + 4 * tid, len = rlen(w);
 #pragma unroll
-            for (int k = 0; k < AGG_ILP; k++) {
-                const u32 i = i0 + k * AGG_NT;
-                u[k] = i < len ? base[i] : 0;
+        for (int k = 0; k < 6; k++) u[k] = i0 + k < len ? u[k] : 0;
+        u64 k0[4], k1[4], c[4];
+        bool v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u32 T = (u32)(u[k] >> 56);
+            const bool head = T >= 0x41;
+            v[k] = T != 0 && (head || (T & 0x1F) < 8);   // skip counts, fillers, medium tails
+            const u64 last = head ? u[k + 1] : u[k];     // unit carrying the count flag
+            k0[k] = head ? u[k] : (u[k] & ~U_CNT);
+            k1[k] = head ? (u[k + 1] & ~U_CNT) : 0;
+            c[k] = (last & U_CNT) ? (head ? u[k + 2] : u[k + 1]) : 1;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k += 2) {
+            typename decltype(tab)::Probe pa, pb;
+            if (v[k]) tab.start(lds_hash(k0[k], k1[k]), pa);
+            if (v[k + 1]) tab.start(lds_hash(k0[k + 1], k1[k + 1]), pb);
+            if (v[k] && !tab.finish(k0[k], k1[k], pa, c[k])) {
+                my_global++;
+                ginsert(a.gtab, a.gmask, k0[k], k1[k], gslot(key_hash(k0[k], k1[k])), c[k], a.st);
             }
-#pragma unroll
-            for (int k = 0; k < AGG_ILP; k += 2) {
-                u64 a0, a1, ac, b0, b1, bc;
-                const bool va = decode(base, i0 + k * AGG_NT, u[k], a0, a1, ac);
-                const bool vb = decode(base, i0 + (k + 1) * AGG_NT, u[k + 1], b0, b1, bc);
-                typename decltype(tab)::Probe pa, pb;
-                if (va) tab.start(lds_hash(a0, a1), pa);
-                if (vb) tab.start(lds_hash(b0, b1), pb);
-                if (va && !tab.finish(a0, a1, pa, ac)) spill(a0, a1, ac);
-                if (vb && !tab.finish(b0, b1, pb, bc)) spill(b0, b1, bc);
+            if (v[k + 1] && !tab.finish(k0[k + 1], k1[k + 1], pb, c[k + 1])) {
+                my_global++;
+                ginsert(a.gtab, a.gmask, k0[k + 1], k1[k + 1], gslot(key_hash(k0[k + 1], k1[k + 1])), c[k + 1], a.st);
             }
         }
+    };
+    u32 wa = w0, ba = (u32)-1;
+    next_batch(wa, ba);
+    u32 wb = wa, bb = ba;
+    next_batch(wb, bb);
+    v4u a0, a1, a2, b0, b1, b2;
+    load(wa, ba, a0, a1, a2);
+    load(wb, bb, b0, b1, b2);
+    while (wa < w1) {
+        process(wa, ba, a0, a1, a2);
+        u32 wn = wb, bn = bb;
+        next_batch(wn, bn);
+        wa = wn; ba = bn;
+        load(wa, ba, a0, a1, a2);
+        if (wb >= w1) break;
+        process(wb, bb, b0, b1, b2);
+        wn = wa; bn = ba;
+        next_batch(wn, bn);
+        wb = wn; bb = bn;
+        load(wb, bb, b0, b1, b2);
     }
     __syncthreads();
     for (int i = tid; i < AGG_NB * 4; i += AGG_NT) {

@@ -304,7 +304,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // the global table
     const u32 P = c->nbuckets;
     u64 per_wg_bytes = (u64)a.tiles_per_wg * MAP_STEP;
-    a.region_cap = std::max<u64>(2048, per_wg_bytes / (8ull * P));
+    a.region_cap = std::max<u64>(2048, per_wg_bytes / (8ull * P)) & ~1ull;   // even: 16-byte aligned regions
     a.pmask = P - 1;
     u64 need = grid * P * a.region_cap * sizeof(u64);
     if (need > c->pool_bytes) {
@@ -340,6 +340,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g.pool = c->pool; g.region_len = c->region_len; g.region_cap = a.region_cap;
     g.P = P; g.nsrc = (u32)grid;
     g.slices = std::max<u32>(1, std::min<u32>((u32)grid, (u32)(c->ncu + P - 1) / P));
+    g.slices = std::max<u32>(g.slices, (u32)((grid + AGG_MAX_SRC - 1) / AGG_MAX_SRC));
     g.gtab = c->gtab; g.gmask = c->gslots - 1; g.st = c->st;
     k_agg<<<P * g.slices, AGG_NT, 0, c->stream>>>(g);
     HIPCHK(c, hipGetLastError());

@@ -17,6 +17,8 @@
 //   5. at the end the workgroup flushes its LDS table into the miss log too.
 // Token ownership: a token belongs to the 16-byte chunk holding its first byte (exactly once).
 #pragma once
+#include <type_traits>
+
 #include "wcg_common.h"
 #include "wcg_lds_table.h"
 
@@ -32,34 +34,6 @@ constexpr int MAP_WNCH = MAP_WREG / 16;
 constexpr int MAP_WMASK = 72;                // mask slots per wave (69 + padding)
 constexpr int MAP_NB = 1576;                 // LDS table buckets (x4 slots, 20 B per slot)
 constexpr int MAX_MISS_BUCKETS = 256;
-
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-typedef int v4i __attribute__((ext_vector_type(4)));
-
-// Streaming input loads are inline-asm buffer loads with hand-counted waits: the compiler's
-// waitcnt pass drains every load (vmcnt(0)) at the top of this loop, which serialises the
-// prefetch.  Rules kept here: each wait names its registers as "+v" so no use moves above it,
-// every asm-loaded register is waited for before it can die or be copied, and N counts only
-// this wave's own younger asm loads (compiler-issued memory ops in between can only make a
-// wait stronger).
-__device__ __forceinline__ v4u buf_load16(v4i rsrc, u32 off) {
-    v4u r;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=&v"(r) : "v"(off), "s"(rsrc) : "memory");
-    return r;
-}
-template <int N>
-__device__ __forceinline__ void buf_wait(v4u& x, v4u& y) {
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(x), "+v"(y) : "n"(N) : "memory");
-}
-__device__ __forceinline__ v4i make_rsrc(const void* base, u32 nbytes) {
-    const u64 p = (u64)base;
-    v4i r;
-    r.x = __builtin_amdgcn_readfirstlane((int)(u32)p);
-    r.y = __builtin_amdgcn_readfirstlane((int)((u32)(p >> 32) & 0xFFFFu));
-    r.z = __builtin_amdgcn_readfirstlane((int)nbytes);
-    r.w = 0x00020000;
-    return r;
-}
 
 struct MapArgs {
     const uint8_t* in;
@@ -199,7 +173,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     // of step 0 and past the end.  Every prefetch is unconditional (the waitcnt pass can only
     // count younger loads that are certainly issued): lanes without an extra chunk and steps
     // past the end load offset 0xFFFFFFF0, which reads zeros without touching memory.
-    auto load = [&](u64 step, v4u& m, v4u& x) {
+    auto load = [&](auto set, u64 step, v4u& m, v4u& x) {      // set: 0 = A registers, 1 = B
         const bool live = step < nsteps;
         const u64 org = (step == 0 || !live) ? 0 : step * MAP_STEP - MAP_PRE;
         const u64 span = live ? a.n - org : 0;
@@ -208,8 +182,13 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         const u32 rel = (u32)(step * MAP_STEP - org);            // 0 for step 0, else 16
         const u32 om = live ? rel + 16 * lane : 0xFFFFFFF0u;
         const u32 ox = (live && xc >= 0) ? rel - MAP_PRE + 16 * xc : 0xFFFFFFF0u;
-        m = buf_load16(rsrc, om);
-        x = buf_load16(rsrc, ox);
+        if constexpr (decltype(set)::value == 0) {
+            m = buf_load16_A0(rsrc, om);
+            x = buf_load16_A1(rsrc, ox);
+        } else {
+            m = buf_load16_B0(rsrc, om);
+            x = buf_load16_B1(rsrc, ox);
+        }
     };
 
     // miss handling shared by both paths
@@ -278,8 +257,8 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         my_tokens += total;
 
-        // ---- tokens, two per lane per iteration (i and i + 64): both tokens' LDS reads, then
-        //      both table probes, are issued before either result is used
+        // ---- tokens, one per lane per iteration (two per lane with both probes in flight was
+        //      measured slower: ~177 tokens per step fill 3 x 64 slots but 2 x 128)
         u32 sink = 0;
         auto token_key = [&](int off, int& len, u64& k0, u64& k1) {
             const int rp = MAP_PRE + off;                       // region position
@@ -300,28 +279,18 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             const u64 b1 = kl > 8 ? (((u64)o3 << 32 | o2) & low_bytes_mask(kl - 8)) : 0ull;
             make_key(b0, b1, kl, k0, k1);
         };
-        for (u32 i = lane; i < total; i += 128) {
-            if (ABL == 1) { sink += sst[i] + (i + 64 < total ? sst[i + 64] : 0); continue; }
-            const bool vb = i + 64 < total;
-            const int offa = sst[i];
-            const int offb = vb ? sst[i + 64] : offa;
-            int la, lb;
-            u64 a0, a1, b0, b1;
-            token_key(offa, la, a0, a1);
-            token_key(offb, lb, b0, b1);
-            const bool sa = la < 16, sb = vb && lb < 16;        // inline keys (fact F4)
-            if (la >= 16) { my_long++; long_token(a, (u64)(base + offa)); }
-            if (vb && lb >= 16) { my_long++; long_token(a, (u64)(base + offb)); }
-            if (ABL == 2) { sink += lds_hash(a0, a1) + lds_hash(b0, b1); continue; }
-            typename decltype(tab)::Probe pa, pb;
-            if (sa) tab.start(lds_hash(a0, a1), pa);
-            if (sb) tab.start(lds_hash(b0, b1), pb);
-            const bool ha = sa && tab.finish(a0, a1, pa, 1u);
-            const bool hb = sb && tab.finish(b0, b1, pb, 1u);
-            if (ABL == 3) { sink += ha + hb; continue; }
-            my_hits += (u32)ha + (u32)hb;
-            if (sa && !ha) miss(a0, a1);
-            if (sb && !hb) miss(b0, b1);
+        for (u32 i = lane; i < total; i += 64) {
+            if (ABL == 1) { sink += sst[i]; continue; }
+            const int off = sst[i];
+            int len;
+            u64 k0, k1;
+            token_key(off, len, k0, k1);
+            if (len >= 16) { my_long++; long_token(a, (u64)(base + off)); continue; }
+            if (ABL == 2) { sink += lds_hash(k0, k1); continue; }
+            const bool hit = tab.add(k0, k1, lds_hash(k0, k1), 1u);
+            if (ABL == 3) { sink += hit; continue; }
+            my_hits += (u32)hit;
+            if (!hit) miss(k0, k1);
         }
         if (ABL) asm volatile("" ::"v"(sink));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -337,21 +306,23 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     auto u4 = [](v4u v) { return make_uint4(v.x, v.y, v.z, v.w); };
     v4u ma, xa, mb, xb;
     u64 st = (u64)blockIdx.x * MAP_WAVES + wave;
-    load(st, ma, xa);
-    load(st + stride, mb, xb);
+    const std::integral_constant<int, 0> SA;
+    const std::integral_constant<int, 1> SB;
+    load(SA, st, ma, xa);
+    load(SB, st + stride, mb, xb);
     while (st < nsteps && !is_tail(st)) {
-        buf_wait<2>(ma, xa);                     // younger: B's two loads
+        buf_wait_A<2>(ma, xa);                   // younger: B's two loads
         process(st, u4(ma), u4(xa));
-        load(st + 2 * stride, ma, xa);
+        load(SA, st + 2 * stride, ma, xa);
         st += stride;
         if (st >= nsteps || is_tail(st)) break;
-        buf_wait<2>(mb, xb);                     // younger: A's two loads
+        buf_wait_B<2>(mb, xb);                   // younger: A's two loads
         process(st, u4(mb), u4(xb));
-        load(st + 2 * stride, mb, xb);
+        load(SB, st + 2 * stride, mb, xb);
         st += stride;
     }
-    buf_wait<0>(ma, xa);                         // nothing may land in a dead register
-    buf_wait<0>(mb, xb);
+    buf_wait_A<0>(ma, xa);                       // nothing may land in a dead register
+    buf_wait_B<0>(mb, xb);
     for (; st < nsteps; st += stride) {
         const long org = (long)(st * MAP_STEP) - MAP_PRE;
         const uint4 mine = load_chunk(a.in, a.n, org + 16 * (lane + 1));

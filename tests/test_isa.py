@@ -1,0 +1,44 @@
+"""Static checks on the gfx950 code of k_map (CPU only: hipcc cross-compiles).
+
+k_map's input stream uses inline-asm loads with hand-counted waits; the compiler must not copy
+those registers between a load and its wait.  tools/check_inflight.py verifies that from the
+generated assembly (tagged loads/waits must all use the same registers), and the kernel must not
+spill to scratch (a scratch reload inside the loop would force a vmcnt(0) that drains the
+prefetch)."""
+import os
+import re
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "mit-6.824-2015_amd", "csrc", "wcg_api.hip")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import check_inflight  # noqa: E402
+
+KMAP0 = "_ZN3wcg5k_mapILi0EEEvNS_7MapArgsE"
+
+
+@pytest.fixture(scope="module")
+def device_asm(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("isa") / "wcg_api.s"
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "--cuda-device-only",
+                        "-S", SRC, "-o", str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return out.read_text()
+
+
+def test_map_asm_loads_not_copied_before_wait(device_asm):
+    errors, loads, waits = check_inflight.check(device_asm, KMAP0)
+    assert not errors, errors
+    assert set(loads) == {"A0", "A1", "B0", "B1"} and len(waits) == 4
+
+
+def test_map_no_scratch(device_asm):
+    lines = check_inflight.kernel_lines(device_asm, KMAP0)
+    assert not any(re.search(r"\bscratch_(load|store)", l) for l in lines)
