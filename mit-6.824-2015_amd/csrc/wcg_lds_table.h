@@ -104,12 +104,75 @@ struct LdsTable {
     }
 };
 
+// k_map's tables: short keys (<= 7 bytes: the k0 word is the whole key, 12 bytes per slot) and
+// medium keys (8-15 bytes: k0 + k1, 20 bytes per slot), each 2 choices x 1 slot.  Measured on
+// the C2 corpus (and a simulation of the same stream): associativity hardly moves the hit rate
+// (2-choice x 1-way 0.678 vs 2-choice x 4-way 0.693 at equal slots) but capacity does, and
+// short keys need 40% less room without a k1 word.  A probe is 2 slots x (k0, k1) loads and
+// compares, the same instructions for both kinds (the table bases are selected per lane; a
+// short key's k1 "slot" is a shared zero word), because k_map is VALU-issue bound and a
+// divergent second probe would cost every wave both.
+template <int NS, int NM>
+struct MapTable {
+    u64* sk0;      // [NS]
+    u32* scnt;     // [NS]
+    u64* mk0;      // [NM]
+    u64* mk1;      // [NM]
+    u32* mcnt;     // [NM]
+    u64* zero;     // one word, always 0
+
+    __device__ __forceinline__ void init(int tid, int nt) {
+        for (int i = tid; i < NS; i += nt) { sk0[i] = 0; scnt[i] = 0; }
+        for (int i = tid; i < NM; i += nt) { mk0[i] = 0; mk1[i] = 0; mcnt[i] = 0; }
+        if (tid == 0) *zero = 0;
+    }
+    // count one occurrence of key (a0, a1) (a1 == 0 for short keys; lds hash h); false = both
+    // candidate slots hold other keys
+    __device__ __forceinline__ bool add(u64 a0, u64 a1, u32 h) {
+        const bool med = !key_short(a0);
+        const u32 n = med ? (u32)NM : (u32)NS;
+        const u32 s1 = __umulhi(h, n), s2 = __umulhi(__builtin_rotateleft32(h, 16), n);
+        u64* K0 = med ? mk0 : sk0;
+        u32* C = med ? mcnt : scnt;
+        const u64* K1a = med ? mk1 + s1 : zero;
+        const u64* K1b = med ? mk1 + s2 : zero;
+        const u64 x1 = K0[s1], x2 = K0[s2], y1 = *K1a, y2 = *K1b;
+        const bool h1 = x1 == a0 && y1 == a1, h2 = x2 == a0 && y2 == a1;
+        if (h1 || h2) {
+            atomicAdd(&C[h1 ? s1 : s2], 1u);
+            return true;
+        }
+        // insert: claim an empty slot's k0, then publish k1 (a reader that sees k0 before k1
+        // treats the slot as another key and may insert a duplicate: harmless, both counts are
+        // flushed and summed downstream)
+        if (x1 == 0) {
+            const u64 old = atomicCAS(&K0[s1], 0ull, a0);
+            if (old == 0) {
+                if (med) mk1[s1] = a1;
+                atomicAdd(&C[s1], 1u);
+                return true;
+            }
+            if (old == a0 && !med) { atomicAdd(&C[s1], 1u); return true; }
+        }
+        if (x2 == 0) {
+            const u64 old = atomicCAS(&K0[s2], 0ull, a0);
+            if (old == 0) {
+                if (med) mk1[s2] = a1;
+                atomicAdd(&C[s2], 1u);
+                return true;
+            }
+            if (old == a0 && !med) { atomicAdd(&C[s2], 1u); return true; }
+        }
+        return false;
+    }
+};
+
 // Hash-derived indices shared by every kernel that touches a key (they must agree):
-//   LDS buckets: lds_hash (LdsTable::buckets)
-//   miss-log bucket and global slot: key_hash, an independent function, so a miss bucket's
-//   keys spread over the whole LDS table of the aggregation kernel.
-//   h2 = key_hash(k0, k1): miss bucket = low bits, global slot = bits 16+
-__device__ __forceinline__ u32 miss_bucket(u64 h2, u32 pmask) { return (u32)h2 & pmask; }
+//   LDS slots / buckets: lds_hash (MapTable::add, LdsTable::buckets, from its high bits)
+//   miss-log bucket: the low bits of lds_hash (k_map has it already; LDS slot choice uses
+//   the high bits, so a miss bucket's keys still spread over k_agg's whole table)
+//   global-table slot: key_hash, an independent 64-bit function, bits 16+
+__device__ __forceinline__ u32 miss_bucket(u32 h, u32 pmask) { return h & pmask; }
 __device__ __forceinline__ u64 gslot(u64 h2) { return h2 >> 16; }
 
 // Miss-log units are 8 bytes; an entry is 1-3 units:

@@ -11,9 +11,10 @@
 //   3. token starts = letter & ~prev_letter (fact F3); the wave compacts them (prefix sum from
 //      4 ballots + mbcnt) into its LDS list and processes them 64 at a time;
 //   4. per token: length from the mask, key identity (<= 15 bytes, fact F4) -> the
-//      workgroup's LDS hash table (exact keys, 2-choice x 4-way buckets, u32 counts); an LDS
-//      miss is appended to this workgroup's region of the miss log (plain stores) for k_agg;
-//      tokens > 15 bytes go to the long-key table with an arena copy of their bytes;
+//      workgroup's LDS tables (exact keys; short and medium keys in separate 2-choice x 1-slot
+//      tables, u32 counts: MapTable); an LDS miss is appended to this workgroup's region of the
+//      miss log (plain stores) for k_agg; tokens > 15 bytes go to the long-key table with an
+//      arena copy of their bytes;
 //   5. at the end the workgroup flushes its LDS table into the miss log too.
 // Token ownership: a token belongs to the 16-byte chunk holding its first byte (exactly once).
 #pragma once
@@ -32,7 +33,8 @@ constexpr int MAP_LOOK = 64;                 // look-ahead bytes (tokens <= 15 n
 constexpr int MAP_WREG = MAP_PRE + MAP_STEP + MAP_LOOK;   // 1104 = 69 chunks
 constexpr int MAP_WNCH = MAP_WREG / 16;
 constexpr int MAP_WMASK = 72;                // mask slots per wave (69 + padding)
-constexpr int MAP_NB = 1576;                 // LDS table buckets (x4 slots, 20 B per slot)
+constexpr int MAP_NS = 8800;                 // LDS short-key slots (12 B each)
+constexpr int MAP_NM = 1024;                 // LDS medium-key slots (20 B each)
 constexpr int MAX_MISS_BUCKETS = 256;
 
 struct MapArgs {
@@ -140,14 +142,17 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     __shared__ __align__(16) uint8_t wbytes[MAP_WAVES][MAP_WREG];
     __shared__ __align__(16) uint16_t wmask[MAP_WAVES][MAP_WMASK];
     __shared__ uint16_t wstart[MAP_WAVES][512];
-    __shared__ __align__(16) u64 tk0[MAP_NB][4];
-    __shared__ __align__(16) u64 tk1[MAP_NB][4];
-    __shared__ u32 tcnt[MAP_NB][4];
+    __shared__ __align__(16) u64 sk0[MAP_NS];
+    __shared__ __align__(16) u64 mk0[MAP_NM];
+    __shared__ __align__(16) u64 mk1[MAP_NM];
+    __shared__ u64 zero_w;
+    __shared__ u32 scnt[MAP_NS];
+    __shared__ u32 mcnt[MAP_NM];
     __shared__ u32 cursor[MAX_MISS_BUCKETS];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);     // wave-uniform (scalar)
-    LdsTable<MAP_NB, u32> tab{tk0, tk1, tcnt};
+    MapTable<MAP_NS, MAP_NM> tab{sk0, scnt, mk0, mk1, mcnt, &zero_w};
     tab.init(tid, MAP_NT);
     for (int i = tid; i < MAX_MISS_BUCKETS; i += MAP_NT) cursor[i] = 0;
     if (lane < MAP_WMASK - MAP_WNCH) wmask[wave][MAP_WNCH + lane] = 0;
@@ -192,11 +197,10 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     };
 
     // miss handling shared by both paths
-    auto miss = [&](u64 k0, u64 k1) {
-        const u64 h2 = key_hash(k0, k1);
-        if (!log_push(a, cursor, miss_bucket(h2, a.pmask), k0, k1, 1u)) {
+    auto miss = [&](u64 k0, u64 k1, u32 h) {
+        if (!log_push(a, cursor, miss_bucket(h, a.pmask), k0, k1, 1u)) {
             my_global++;
-            ginsert(a.gtab, a.gmask, k0, k1, gslot(h2), 1, a.st);
+            ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
         }
     };
 
@@ -286,11 +290,12 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             u64 k0, k1;
             token_key(off, len, k0, k1);
             if (len >= 16) { my_long++; long_token(a, (u64)(base + off)); continue; }
-            if (ABL == 2) { sink += lds_hash(k0, k1); continue; }
-            const bool hit = tab.add(k0, k1, lds_hash(k0, k1), 1u);
+            const u32 h = lds_hash(k0, k1);
+            if (ABL == 2) { sink += h; continue; }
+            const bool hit = tab.add(k0, k1, h);
             if (ABL == 3) { sink += hit; continue; }
             my_hits += (u32)hit;
-            if (!hit) miss(k0, k1);
+            if (!hit) miss(k0, k1, h);
         }
         if (ABL) asm volatile("" ::"v"(sink));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -333,16 +338,15 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     // ---- flush the LDS table into this workgroup's miss-log regions (entries with counts);
     //      a full region -> global table
     __syncthreads();
-    for (int i = tid; i < MAP_NB * 4; i += MAP_NT) {
-        const u32 c = (&tcnt[0][0])[i];
-        if (!c) continue;
-        const u64 k0 = (&tk0[0][0])[i], k1 = (&tk1[0][0])[i];
-        const u64 h2 = key_hash(k0, k1);
-        if (!log_push(a, cursor, miss_bucket(h2, a.pmask), k0, k1, c)) {
+    auto flush = [&](u64 k0, u64 k1, u32 c) {
+        if (!c) return;
+        if (!log_push(a, cursor, miss_bucket(lds_hash(k0, k1), a.pmask), k0, k1, c)) {
             my_global++;
-            ginsert(a.gtab, a.gmask, k0, k1, gslot(h2), c, a.st);
+            ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
         }
-    }
+    };
+    for (int i = tid; i < MAP_NS; i += MAP_NT) flush(sk0[i], 0, scnt[i]);
+    for (int i = tid; i < MAP_NM; i += MAP_NT) flush(mk0[i], mk1[i], mcnt[i]);
     __syncthreads();
     for (u32 p = tid; p <= a.pmask; p += MAP_NT) {
         const u32 c = cursor[p];
