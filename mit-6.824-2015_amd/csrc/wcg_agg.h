@@ -14,7 +14,7 @@ namespace wcg {
 
 constexpr int AGG_NT = 1024;
 constexpr u32 AGG_BATCH = AGG_NT * 4;     // units per batch (4 per thread)
-constexpr int AGG_NB = 1696;           // 1696 x 4 slots x 24 B (u64 counts) = 162816 B
+constexpr int AGG_NB = 1690;           // 1690 x 4 slots x 24 B (u64 counts) = 162240 B (+ 1.5 KiB)
 constexpr u32 AGG_MAX_SRC = 256;       // source regions per workgroup (+1 KiB LDS = 160 KiB)
 
 struct AggArgs {
@@ -27,6 +27,7 @@ struct AggArgs {
     GEntry* gtab;
     u64 gmask;
     DevState* st;
+    const u64* map_stats;  // k_map's per-workgroup stats [nsrc][4], summed by workgroup 0
 };
 
 __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
@@ -124,8 +125,21 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
         my_global++;
         ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
     }
+    // one atomic per workgroup (a per-wave atomic on one DevState line serialises)
+    __shared__ u64 wsum[AGG_NT / 64][4];
     for (int d = 32; d >= 1; d >>= 1) my_global += __shfl_xor(my_global, d, 64);
-    if ((tid & 63) == 0) atomicAdd(&a.st->global_ops, my_global);
+    u64 ms = 0;
+    if (blockIdx.x == 0)                       // k_map's stats: tokens, lds hits, global ops, long
+        for (u32 w = tid >> 2; w < a.nsrc; w += AGG_NT / 4) ms += a.map_stats[(u64)w * 4 + (tid & 3)];
+    for (int d = 32; d >= 4; d >>= 1) ms += __shfl_xor(ms, d, 64);
+    if ((tid & 63) < 4) wsum[tid >> 6][tid & 3] = ms + ((tid & 63) == 2 ? my_global : 0);
+    __syncthreads();
+    if (tid < 4) {
+        u64 t = 0;
+        for (int w = 0; w < AGG_NT / 64; w++) t += wsum[w][tid];
+        u64* dst[4] = {&a.st->tokens, &a.st->lds_hits, &a.st->global_ops, &a.st->long_tokens};
+        if (t) atomicAdd(dst[tid], t);
+    }
 }
 
 }  // namespace wcg

@@ -49,6 +49,7 @@ struct wcg_ctx {
     // miss log (k_map -> k_agg)
     u64* pool = nullptr; u64 pool_bytes = 0;
     u32* region_len = nullptr; u64 region_len_cap = 0;
+    u64* wg_stats = nullptr; u64 wg_stats_cap = 0;   // k_map per-workgroup stats [grid][4]
     u32 nbuckets = 64;
     // timing
     bool timing = false;
@@ -243,7 +244,7 @@ int wcg_close(wcg_ctx* c) {
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     void* bufs[] = {c->d_in, c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens,
                     c->d_scalar, c->d_out, c->d_part, c->owner, c->d_per_rank, c->exp_buf,
-                    c->pool, c->region_len};
+                    c->pool, c->region_len, c->wg_stats};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
@@ -291,7 +292,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     MapArgs a;
     a.in = (const uint8_t*)dev_bytes;
     a.n = n;
-    a.ntiles = (n + MAP_STEP - 1) / MAP_STEP;      // 1 KiB wave steps
+    a.ntiles = (n + MAP_STEP - 1) / MAP_STEP;      // 992-byte wave steps (1 KiB windows)
     // one workgroup per CU (LDS-bound); steps are dealt chip-wide inside the kernel
     u64 grid = std::min<u64>((u64)c->ncu, (a.ntiles + MAP_WAVES - 1) / MAP_WAVES);
     a.tiles_per_wg = (a.ntiles + grid - 1) / grid;          // steps per workgroup (sizing only)
@@ -321,8 +322,16 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         HIPCHK(c, hipMalloc(&c->region_len, grid * P * sizeof(u32)));
         c->region_len_cap = grid * P;
     }
+    if (grid > c->wg_stats_cap) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->wg_stats) HIPCHK(c, hipFree(c->wg_stats));
+        c->wg_stats = nullptr; c->wg_stats_cap = 0;
+        HIPCHK(c, hipMalloc(&c->wg_stats, grid * 4 * sizeof(u64)));
+        c->wg_stats_cap = grid;
+    }
     a.pool = c->pool;
     a.region_len = c->region_len;
+    a.wg_stats = c->wg_stats;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (c->timing) { e0 = take_event(c); HIPCHK(c, hipEventRecord(e0, c->stream)); }
     static const int ablate = getenv("WCG_MAP_ABLATE") ? atoi(getenv("WCG_MAP_ABLATE")) : 0;
@@ -342,6 +351,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g.slices = std::max<u32>(1, std::min<u32>((u32)grid, (u32)(c->ncu + P - 1) / P));
     g.slices = std::max<u32>(g.slices, (u32)((grid + AGG_MAX_SRC - 1) / AGG_MAX_SRC));
     g.gtab = c->gtab; g.gmask = c->gslots - 1; g.st = c->st;
+    g.map_stats = c->wg_stats;
     k_agg<<<P * g.slices, AGG_NT, 0, c->stream>>>(g);
     HIPCHK(c, hipGetLastError());
     if (c->timing) {

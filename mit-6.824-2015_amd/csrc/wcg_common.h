@@ -140,14 +140,18 @@ __device__ __host__ __forceinline__ u64 mix64(u64 x) {
 __device__ __forceinline__ u64 key_hash(u64 k0, u64 k1) {
     return mix64(k0 * 0x9E3779B97F4A7C15ull + (k1 ^ (k1 >> 29)) * 0xC2B2AE3D27D4EB4Full);
 }
-// 32-bit key hash for the LDS tables (two 32-bit multiplies on the hot path)
-__device__ __forceinline__ u32 lds_hash(u64 k0, u64 k1) {
-    u32 x = (u32)k0 ^ __builtin_rotateleft32((u32)(k0 >> 32), 11) ^ __builtin_rotateleft32((u32)k1, 19) ^
-            __builtin_rotateleft32((u32)(k1 >> 32), 27);
-    x ^= x >> 16; x *= 0x7FEB352Du;
-    x ^= x >> 15; x *= 0x846CA68Bu;
-    x ^= x >> 16;
+// 32-bit key hash for the LDS tables and the miss-log bucket: the four key words folded with
+// rotations, then one multiply between two xor-shifts (one quarter-rate multiply on k_map's hot
+// path; the multiply mixes low bits up, the final shift brings high bits down to the bucket bits)
+__device__ __forceinline__ u32 lds_hash32(u32 a, u32 b, u32 c, u32 d) {
+    u32 x = a ^ __builtin_rotateleft32(b, 9) ^ __builtin_rotateleft32(c, 17) ^ __builtin_rotateleft32(d, 25);
+    x ^= x >> 15;
+    x *= 0x2C1B3C6Du;
+    x ^= x >> 12;
     return x;
+}
+__device__ __forceinline__ u32 lds_hash(u64 k0, u64 k1) {
+    return lds_hash32((u32)k0, (u32)(k0 >> 32), (u32)k1, (u32)(k1 >> 32));
 }
 __device__ __forceinline__ u32 fnv1a_step(u32 h, u32 byte) { return (h ^ byte) * 0x01000193u; }
 

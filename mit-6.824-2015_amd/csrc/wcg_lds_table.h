@@ -126,42 +126,55 @@ struct MapTable {
         for (int i = tid; i < NM; i += nt) { mk0[i] = 0; mk1[i] = 0; mcnt[i] = 0; }
         if (tid == 0) *zero = 0;
     }
-    // count one occurrence of key (a0, a1) (a1 == 0 for short keys; lds hash h); false = both
-    // candidate slots hold other keys
-    __device__ __forceinline__ bool add(u64 a0, u64 a1, u32 h) {
-        const bool med = !key_short(a0);
-        const u32 n = med ? (u32)NM : (u32)NS;
-        const u32 s1 = __umulhi(h, n), s2 = __umulhi(__builtin_rotateleft32(h, 16), n);
+    // slot choices from 16-bit fields of h by full-rate 24-bit multiplies (bits 16-31 and
+    // 6-21; bits 0-5 are the miss bucket, so a bucket's keys still spread over both choices)
+    __device__ __forceinline__ static void slots(u32 h, u32 n, u32& s1, u32& s2) {
+        s1 = __umul24(h >> 16, n) >> 16;
+        s2 = __umul24((h >> 6) & 0xFFFFu, n) >> 16;
+    }
+    // A probe split in two so that k_map can issue its reads together with the next token's:
+    // probe() computes the candidate slots and reads them, finish() counts one occurrence of
+    // key (a0, a1) (a1 == 0 for short keys) when `valid` and returns true on a hit or insert,
+    // false = both candidate slots hold other keys.  One divergent branch on the hit path (the
+    // count add); the insert path (a probe saw an empty slot) is rare once the table has filled.
+    struct Probe { u32 s1, s2; u64 x1, x2, y1, y2; };
+    __device__ __forceinline__ Probe probe(bool med, u32 h) const {
+        static_assert(NS < 65536 && NM < 65536, "24-bit slot multiply");
+        Probe p;
+        slots(h, med ? (u32)NM : (u32)NS, p.s1, p.s2);
+        const u64* K0 = med ? mk0 : sk0;
+        const u64* K1a = med ? mk1 + p.s1 : zero;
+        const u64* K1b = med ? mk1 + p.s2 : zero;
+        p.x1 = K0[p.s1]; p.x2 = K0[p.s2]; p.y1 = *K1a; p.y2 = *K1b;
+        return p;
+    }
+    __device__ __forceinline__ bool finish(bool valid, bool med, u64 a0, u64 a1, const Probe& p) {
         u64* K0 = med ? mk0 : sk0;
         u32* C = med ? mcnt : scnt;
-        const u64* K1a = med ? mk1 + s1 : zero;
-        const u64* K1b = med ? mk1 + s2 : zero;
-        const u64 x1 = K0[s1], x2 = K0[s2], y1 = *K1a, y2 = *K1b;
-        const bool h1 = x1 == a0 && y1 == a1, h2 = x2 == a0 && y2 == a1;
-        if (h1 || h2) {
-            atomicAdd(&C[h1 ? s1 : s2], 1u);
-            return true;
-        }
+        const bool h1 = p.x1 == a0 && p.y1 == a1, h2 = p.x2 == a0 && p.y2 == a1;
+        const bool hit = valid && (h1 || h2);
+        if (hit) atomicAdd(&C[h1 ? p.s1 : p.s2], 1u);
+        if (!valid || hit || (p.x1 != 0 && p.x2 != 0)) return hit;
         // insert: claim an empty slot's k0, then publish k1 (a reader that sees k0 before k1
         // treats the slot as another key and may insert a duplicate: harmless, both counts are
         // flushed and summed downstream)
-        if (x1 == 0) {
-            const u64 old = atomicCAS(&K0[s1], 0ull, a0);
+        if (p.x1 == 0) {
+            const u64 old = atomicCAS(&K0[p.s1], 0ull, a0);
             if (old == 0) {
-                if (med) mk1[s1] = a1;
-                atomicAdd(&C[s1], 1u);
+                if (med) mk1[p.s1] = a1;
+                atomicAdd(&C[p.s1], 1u);
                 return true;
             }
-            if (old == a0 && !med) { atomicAdd(&C[s1], 1u); return true; }
+            if (old == a0 && !med) { atomicAdd(&C[p.s1], 1u); return true; }
         }
-        if (x2 == 0) {
-            const u64 old = atomicCAS(&K0[s2], 0ull, a0);
+        if (p.x2 == 0) {
+            const u64 old = atomicCAS(&K0[p.s2], 0ull, a0);
             if (old == 0) {
-                if (med) mk1[s2] = a1;
-                atomicAdd(&C[s2], 1u);
+                if (med) mk1[p.s2] = a1;
+                atomicAdd(&C[p.s2], 1u);
                 return true;
             }
-            if (old == a0 && !med) { atomicAdd(&C[s2], 1u); return true; }
+            if (old == a0 && !med) { atomicAdd(&C[p.s2], 1u); return true; }
         }
         return false;
     }

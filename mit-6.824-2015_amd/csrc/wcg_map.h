@@ -1,22 +1,36 @@
 // wcg_map.h - the map kernel: DoMap + Map (mapreduce.go:193-231, wc.go:17-30) on gfx950.
 //
-// One workgroup (16 waves) per CU owns a contiguous range of 1 KiB steps; wave w of the
-// workgroup processes steps w, w+16, w+32, ... of that range on its own - its own LDS slice,
-// no workgroup barrier in the main loop, so the 16 waves overlap each other's latencies:
-//   1. every lane loads one 16-byte chunk of the step (one coalesced 1 KiB dwordx4 load per
-//      wave), lanes 0-4 also the 16-byte prefix and the 64-byte look-ahead that lets tokens
-//      crossing the step end be read whole; the loads run 2 steps ahead in registers;
-//   2. per chunk: 16-bit letter-byte mask - SWAR on all-ASCII chunks (fact F2), Go UTF-8
-//      decode + Unicode-13 letter bitmap otherwise (fact F1);
-//   3. token starts = letter & ~prev_letter (fact F3); the wave compacts them (prefix sum from
-//      4 ballots + mbcnt) into its LDS list and processes them 64 at a time;
-//   4. per token: length from the mask, key identity (<= 15 bytes, fact F4) -> the
-//      workgroup's LDS tables (exact keys; short and medium keys in separate 2-choice x 1-slot
-//      tables, u32 counts: MapTable); an LDS miss is appended to this workgroup's region of the
-//      miss log (plain stores) for k_agg; tokens > 15 bytes go to the long-key table with an
-//      arena copy of their bytes;
+// One workgroup (16 waves) per CU.  Wave w of workgroup g processes the steps
+// g*16 + w + k*(G*16), k = 0, 1, ... on its own (no workgroup barrier in the main loop).  A step
+// is 62 chunks of 16 bytes (992 input bytes); the wave loads the 1 KiB window that starts one
+// chunk before it, so lane 0 holds the prefix chunk, lanes 1-62 the step's own chunks and lane
+// 63 the look-ahead chunk - one coalesced 1 KiB buffer load per wave, no extra loads:
+//   1. MAP_SETS windows are in flight per wave (register sets A-D, waits counted exactly: see
+//      "prefetch accounting" below);
+//   2. the window is staged in the wave's LDS slice (key bytes and UTF-8 context only: every
+//      lane computes its chunk's letter mask from registers - SWAR on all-ASCII chunks (fact
+//      F2), Go UTF-8 decode + Unicode-13 letter bitmap otherwise (fact F1));
+//   3. token starts = letter & ~prev_letter (fact F3) with the neighbour chunks' masks taken by
+//      DPP lane shifts; each start's run length is read off the 32-bit mask window (own | next);
+//      the wave compacts {offset, length} entries (prefix sum from 4 ballots + mbcnt) into its
+//      LDS list;
+//   4. tokens, 64 per uniform iteration: key identity (<= 15 bytes, fact F4) from two unaligned
+//      8-byte LDS reads -> the workgroup's LDS tables (exact keys, short and medium keys in
+//      2-choice x 1-slot tables, u32 counts: MapTable); a miss is appended to this workgroup's
+//      region of the miss log for k_agg; tokens > 15 bytes go to the long-key table with an
+//      arena copy of their bytes (global memory path);
 //   5. at the end the workgroup flushes its LDS table into the miss log too.
-// Token ownership: a token belongs to the 16-byte chunk holding its first byte (exactly once).
+// Token ownership: a token belongs to the 16-byte chunk holding its first byte (exactly once);
+// only lanes 1-62 own chunks.
+//
+// Prefetch accounting.  `s_waitcnt vmcnt(N)` waits until all but this wave's N youngest vector
+// memory operations are done (loads and stores retire in issue order).  A step's processing
+// issues exactly 2 miss-log stores per token iteration plus 2 after its last one (inline-asm
+// buffer stores executed by the whole wave, out-of-range offsets for lanes without a miss), so
+// when set s is due the number of operations issued after its loads is known: 2 loads +
+// 2 * (iters + 1) for each of the MAP_SETS - 1 steps processed since.  The wait uses the largest quantised N not above that
+// count; any operation the count does not know about (rare paths: long tokens, a full miss-log
+// region, UTF-8 table loads) can only make the wait stronger.
 #pragma once
 #include <type_traits>
 
@@ -27,15 +41,19 @@ namespace wcg {
 
 constexpr int MAP_NT = 1024;                 // threads per workgroup
 constexpr int MAP_WAVES = MAP_NT / 64;       // 16 independent waves
-constexpr int MAP_STEP = 1024;               // bytes per wave step (64 lanes x 16 B)
-constexpr int MAP_PRE = 16;                  // prefix bytes (need 4)
-constexpr int MAP_LOOK = 64;                 // look-ahead bytes (tokens <= 15 need 15)
-constexpr int MAP_WREG = MAP_PRE + MAP_STEP + MAP_LOOK;   // 1104 = 69 chunks
-constexpr int MAP_WNCH = MAP_WREG / 16;
-constexpr int MAP_WMASK = 72;                // mask slots per wave (69 + padding)
-constexpr int MAP_NS = 8800;                 // LDS short-key slots (12 B each)
+constexpr int MAP_OWN = 62;                  // chunks owned per step (lanes 1-62)
+constexpr int MAP_STEP = 16 * MAP_OWN;       // 992 input bytes per wave step
+constexpr int MAP_WIN = 1024;                // bytes loaded per step: [step base - 16, + 1024)
+constexpr int MAP_WREG = MAP_WIN + 8;        // staging (+8: keyread's third word at the end)
+constexpr int MAP_SST = 512;                 // max token starts per step (992 / 2 = 496)
+constexpr int MAP_NS = 8960;                 // LDS short-key slots (12 B each)
 constexpr int MAP_NM = 1024;                 // LDS medium-key slots (20 B each)
+#ifndef WCG_MAP_SETS
+#define WCG_MAP_SETS 4
+#endif
+constexpr int MAP_SETS = WCG_MAP_SETS;       // steps in flight per wave (2 or 4)
 constexpr int MAX_MISS_BUCKETS = 256;
+constexpr u32 SST_LEN_SHIFT = 10;            // start entry = window offset | min(run, 16) << 10
 
 struct MapArgs {
     const uint8_t* in;
@@ -49,6 +67,7 @@ struct MapArgs {
     u64* pool;     u64 region_cap;  // miss log: region (wg, p) = pool[(wg * P + p) * region_cap ...]
     u32* region_len;               // units written per region
     u32 pmask;                     // P - 1 (P = number of miss buckets, power of two)
+    u64* wg_stats;                 // [grid][4] per-workgroup {tokens, lds hits, global ops, long}
 };
 
 // append one miss-log entry (wcg_lds_table.h) for this workgroup; false when the region is
@@ -81,7 +100,8 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* in, u64 n, long pos) 
     return v;
 }
 
-// long token (> 15 bytes) starting at absolute offset p: walk runes in global memory
+// long token (> 15 bytes, or a run k_map could not measure in its window) starting at absolute
+// offset p: walk runes in global memory
 __device__ void long_token(const MapArgs& a, u64 p) {
     const uint8_t* in = a.in;
     u64 n = a.n;
@@ -96,6 +116,19 @@ __device__ void long_token(const MapArgs& a, u64 p) {
         q += w;
     }
     u64 len = q - p;
+    if (len <= 15) {
+        // a run k_map could not measure inside its window (a UTF-8 look-ahead chunk) that turns
+        // out to be an inline key: count it in the inline-key table like any other
+        u64 b0 = 0, b1 = 0;
+        for (u64 i = 0; i < len; i++) {
+            if (i < 8) b0 |= (u64)in[p + i] << (8 * i);
+            else b1 |= (u64)in[p + i] << (8 * (i - 8));
+        }
+        u64 k0, k1;
+        make_key(b0, b1, (int)len, k0, k1);
+        ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
+        return;
+    }
     if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); return; }
     u64 tag = mix64(h ^ len) | 1ull;
     u64 s = tag & a.lmask, probes = 0;
@@ -134,14 +167,68 @@ __device__ void long_token(const MapArgs& a, u64 p) {
     }
 }
 
+// 16-bit letter mask of the region chunk at byte `pos` of the wave's staged bytes (UTF-8 path)
+template <typename At>
+__device__ __forceinline__ u32 utf8_mask(At at, int pos, int from) {
+    u32 m = 0;
+#pragma unroll 1
+    for (int i = from; i < 16; i++)
+        if (letter_byte(at, (long)(pos + i))) m |= 1u << i;
+    return m;
+}
+
+// wave-local ordering of LDS accesses between lanes (the LDS executes one wave's
+// instructions in order; this keeps the compiler from moving accesses across)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- prefetch registers: tagged asm loads per set (tools/check_inflight.py) and waits with a
+//      quantised count (largest listed value <= n; n counts operations younger than the set)
+// the quantised wait as ONE asm statement (a chain of scalar compares and branches around
+// s_waitcnt): one asm keeps the set's registers in place (a chain of C++ branches, each with
+// its own asm, makes the compiler merge their outputs through register copies)
+#define WCG_W1(N, L) "s_cmp_ge_u32 %1, " #N "\n\ts_cbranch_scc0 " #L "f\n\ts_waitcnt vmcnt(" #N ")\n\ts_branch 99f\n" #L ":\n\t"
+#define WCG_WAIT_CHAIN(TAG)                                                                     \
+    WCG_W1(48, 81) WCG_W1(36, 82) WCG_W1(28, 83) WCG_W1(22, 84) WCG_W1(18, 85) WCG_W1(14, 86)   \
+    WCG_W1(12, 87) WCG_W1(10, 88) WCG_W1(8, 89) WCG_W1(6, 90) WCG_W1(4, 91) WCG_W1(2, 92)        \
+    "s_waitcnt vmcnt(0)\n99: ; " TAG
+#define WCG_SET_OPS(S)                                                                          \
+    __device__ __forceinline__ void set_load_##S(v4i rsrc, u32 om, v4u& m) {                    \
+        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen ; wcg-load " #S "0"               \
+                     : "=&v"(m) : "v"(om), "s"(rsrc) : "memory");                               \
+    }                                                                                           \
+    template <int N>                                                                            \
+    __device__ __forceinline__ void set_wait_n_##S(v4u& m) {                                    \
+        asm volatile("s_waitcnt vmcnt(%1) ; wcg-wait " #S " %0" : "+v"(m) : "n"(N) : "memory"); \
+    }                                                                                           \
+    __device__ __forceinline__ void set_wait_##S(u32 n, v4u& m) {                               \
+        asm volatile(WCG_WAIT_CHAIN("wcg-wait " #S " %0") : "+v"(m) : "s"(n) : "memory", "scc"); \
+    }
+
+WCG_SET_OPS(A)
+WCG_SET_OPS(B)
+WCG_SET_OPS(C)
+WCG_SET_OPS(D)
+#undef WCG_SET_OPS
+static_assert(MAP_SETS == 2 || MAP_SETS == 4, "k_map's main loop names two or four register sets");
+
+// one miss-log unit store issued by the whole wave (lanes without a unit pass an out-of-range
+// offset: the buffer range check drops the write); counted by the prefetch accounting
+__device__ __forceinline__ void unit_store(v4i rsrc, u32 off, u64 v) {
+    asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen ; wcg-store" :: "v"(v), "v"(off), "s"(rsrc) : "memory");
+}
+constexpr u32 OOB = 0xFFFFFFF0u;
+
 // ABL (measurement builds only, selected by WCG_MAP_ABLATE; results are wrong when ABL != 0):
 //   5 = input loads only, 4 = + LDS staging and letter masks, 1 = + token starts and compaction,
 //   2 = + key extraction and hash, 3 = + LDS lookup with misses dropped
 template <int ABL>
 __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     __shared__ __align__(16) uint8_t wbytes[MAP_WAVES][MAP_WREG];
-    __shared__ __align__(16) uint16_t wmask[MAP_WAVES][MAP_WMASK];
-    __shared__ uint16_t wstart[MAP_WAVES][512];
+    __shared__ __align__(16) uint16_t wstart[MAP_WAVES][MAP_SST];
     __shared__ __align__(16) u64 sk0[MAP_NS];
     __shared__ __align__(16) u64 mk0[MAP_NM];
     __shared__ __align__(16) u64 mk1[MAP_NM];
@@ -155,94 +242,98 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     MapTable<MAP_NS, MAP_NM> tab{sk0, scnt, mk0, mk1, mcnt, &zero_w};
     tab.init(tid, MAP_NT);
     for (int i = tid; i < MAX_MISS_BUCKETS; i += MAP_NT) cursor[i] = 0;
-    if (lane < MAP_WMASK - MAP_WNCH) wmask[wave][MAP_WNCH + lane] = 0;
     __syncthreads();
 
     uint8_t* const bytes = wbytes[wave];
-    uint16_t* const msk = wmask[wave];
     uint16_t* const sst = wstart[wave];
     // Steps are dealt chip-wide: wave w of workgroup g takes steps (g * 16 + w) + k * G * 16, so
     // the chip sweeps the input front to back (HBM-friendly) while every workgroup still sees
     // a uniform sample of it for its LDS table.
     const u64 nsteps = a.ntiles;
     const u64 stride = (u64)gridDim.x * MAP_WAVES;
-    // region chunk c <-> input bytes [step_base - PRE + 16c, +16): lane owns chunk lane+1;
-    // lane 0 also chunk 0 (prefix), lane 63 chunk 65 (first look-ahead chunk, its DPP "next"),
-    // lanes 1-3 chunks 66-68 (rest of the 64-byte look-ahead used by the UTF-8 path)
-    const int xc = (lane == 0) ? 0 : (lane == 63 ? 65 : (lane <= 3 ? 65 + lane : -1));
+    // window chunk c <-> input bytes [step base - 16 + 16c, +16); lane c holds chunk c
     u64 my_tokens = 0;                           // wave-uniform
     u32 my_hits = 0, my_global = 0, my_long = 0;
 
-    // Input loads: raw buffer loads through a per-step descriptor based at the step's prefix
-    // (at the input start for step 0); the hardware range check returns zeros for the prefix
-    // of step 0 and past the end.  Every prefetch is unconditional (the waitcnt pass can only
-    // count younger loads that are certainly issued): lanes without an extra chunk and steps
-    // past the end load offset 0xFFFFFFF0, which reads zeros without touching memory.
-    auto load = [&](auto set, u64 step, v4u& m, v4u& x) {      // set: 0 = A registers, 1 = B
+    // miss-log stores of this workgroup: one buffer resource over its regions
+    const u32 P = a.pmask + 1;
+    u64* const wpool = a.pool + (u64)blockIdx.x * P * a.region_cap;
+    const v4i prsrc = make_rsrc(wpool, (u32)(P * a.region_cap * 8));
+
+    // Input loads: raw buffer loads through a per-step descriptor based at the window start
+    // (at the input start for step 0, whose prefix chunk is out of range and reads zeros).
+    // Every prefetch is unconditional: steps past the end load offset 0xFFFFFFF0, which reads
+    // zeros without touching memory.
+    auto addr = [&](u64 step, v4i& rsrc, u32& om) {
         const bool live = step < nsteps;
-        const u64 org = (step == 0 || !live) ? 0 : step * MAP_STEP - MAP_PRE;
+        const u64 org = (step == 0 || !live) ? 0 : step * MAP_STEP - 16;
         const u64 span = live ? a.n - org : 0;
         const u32 nrec = span > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)span;
-        const v4i rsrc = make_rsrc(a.in + org, nrec);
-        const u32 rel = (u32)(step * MAP_STEP - org);            // 0 for step 0, else 16
-        const u32 om = live ? rel + 16 * lane : 0xFFFFFFF0u;
-        const u32 ox = (live && xc >= 0) ? rel - MAP_PRE + 16 * xc : 0xFFFFFFF0u;
-        if constexpr (decltype(set)::value == 0) {
-            m = buf_load16_A0(rsrc, om);
-            x = buf_load16_A1(rsrc, ox);
+        rsrc = make_rsrc(a.in + org, nrec);
+        const u32 rel = step == 0 ? 0u : 16u;
+        om = live ? 16 * lane + rel - 16 : OOB;                  // step 0, lane 0: wraps to OOB
+    };
+
+    // ---- token decoding.  An entry of the start list -> the key's 16 bytes from three aligned
+    //      8-byte LDS reads (unaligned 8-byte LDS reads cost ~20x the LDS cycles), then the key
+    //      identity of fact F4 with byte masks, and its LDS hash
+    struct KeyWords { uint2 q0, q1, q2; };
+    struct Tok { u32 e, k0l, k0h, k1l, k1h, h; bool shrt, lng, valid; };
+    auto keyread = [&](u32 e) -> KeyWords {
+        const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1);
+        const uint2* q = reinterpret_cast<const uint2*>(bytes + (rp & ~7u));
+        return KeyWords{q[0], q[1], q[2]};
+    };
+    auto decode_tok = [&](u32 e, bool act, const KeyWords& kw) -> Tok {
+        Tok t;
+        t.e = e;
+        const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1), len = e >> SST_LEN_SHIFT;
+        const u32 bsh = rp & 3u;
+        const bool hi4 = (rp & 4u) != 0;
+        const u32 e0 = hi4 ? kw.q0.y : kw.q0.x, e1 = hi4 ? kw.q1.x : kw.q0.y, e2 = hi4 ? kw.q1.y : kw.q1.x;
+        const u32 e3 = hi4 ? kw.q2.x : kw.q1.y, e4 = hi4 ? kw.q2.y : kw.q2.x;
+        const u32 w0 = __builtin_amdgcn_alignbyte(e1, e0, bsh), w1 = __builtin_amdgcn_alignbyte(e2, e1, bsh);
+        const u32 w2 = __builtin_amdgcn_alignbyte(e3, e2, bsh), w3 = __builtin_amdgcn_alignbyte(e4, e3, bsh);
+        // keep the key's bytes: nb = bytes in the last (partial) word pair, 0..7
+        t.shrt = len < 8;
+        const u32 nb = t.shrt ? len : len - 8;
+        const u32 ml = nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1;
+        const u32 mh = nb >= 4 ? (1u << (8 * nb - 32)) - 1 : 0u;
+        const u32 pl = (t.shrt ? w0 : w2) & ml;
+        const u32 ph = ((t.shrt ? w1 : w3) & mh) | (len << 24);
+        t.k0l = t.shrt ? pl : w0; t.k0h = t.shrt ? ph : w1;
+        t.k1l = t.shrt ? 0u : pl; t.k1h = t.shrt ? 0u : ph;
+        t.lng = act && len >= 16;
+        t.valid = act && len < 16;
+        t.h = lds_hash32(t.k0l, t.k0h, t.k1l, t.k1h);
+        return t;
+    };
+
+    // one step: returns the number of unit-store pairs it issued (prefetch accounting)
+    auto process = [&](u64 step, const uint4 mine) -> u32 {
+        const long wbase = (long)(step * MAP_STEP) - 16;        // input offset of window byte 0
+        if (ABL == 5) { asm volatile("" ::"v"(mine.x)); return 0; }
+        reinterpret_cast<uint4*>(bytes)[lane] = mine;
+        // ---- letter mask of the lane's chunk (lane 0: only bit 15 is used - the predecessor of
+        //      the step's first byte; lane 63: only as the successor of chunk 62, and on the
+        //      UTF-8 path its last 3 bits, whose runes may end past the window, are forced to
+        //      letters, so a run reaching them is measured exactly by the long-token path)
+        u32 m;
+        if (all_ascii(mine)) {
+            m = ascii_mask16(mine);
         } else {
-            m = buf_load16_B0(rsrc, om);
-            x = buf_load16_B1(rsrc, ox);
+            wave_lds_sync();
+            auto at = [&](long i) -> u32 { return (i >= 0 && i < MAP_WIN) ? (u32)bytes[i] : 0u; };
+            m = utf8_mask(at, 16 * lane, lane == 0 ? 12 : 0);
+            if (lane == 63) m |= 0xE000u;
         }
-    };
-
-    // miss handling shared by both paths
-    auto miss = [&](u64 k0, u64 k1, u32 h) {
-        if (!log_push(a, cursor, miss_bucket(h, a.pmask), k0, k1, 1u)) {
-            my_global++;
-            ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
-        }
-    };
-
-    auto process = [&](u64 step, const uint4 mine, const uint4 extra) {
-        const long base = (long)(step * MAP_STEP);
-        if (ABL == 5) { asm volatile("" ::"v"(mine.x ^ extra.y)); return; }
-        reinterpret_cast<uint4*>(bytes)[lane + 1] = mine;
-        if (xc >= 0) reinterpret_cast<uint4*>(bytes)[xc] = extra;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // ---- letter masks
-        auto at = [&](long i) -> u32 { return (i >= 0 && i < MAP_WREG) ? (u32)bytes[i] : 0u; };
-        {
-            u32 m;
-            if (all_ascii(mine)) {
-                m = ascii_mask16(mine);
-            } else {
-                m = 0;
-                for (int i = 0; i < 16; i++)
-                    if (letter_byte(at, (long)(16 * (lane + 1) + i))) m |= 1u << i;
-            }
-            msk[lane + 1] = (uint16_t)m;
-            if (xc >= 0) {
-                if (all_ascii(extra)) {
-                    m = ascii_mask16(extra);
-                } else {
-                    m = 0;
-                    for (int i = (xc == 0 ? 4 : 0); i < 16; i++)   // prefix chunk: only its tail matters
-                        if (letter_byte(at, (long)(16 * xc + i))) m |= 1u << i;
-                }
-                msk[xc] = (uint16_t)m;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (ABL == 4) { asm volatile("" ::"v"((u32)msk[lane + 1])); return; }
-        // ---- token starts in my chunk; wave prefix sum of the counts (<= 8) from 4 ballots
-        const u32 m = msk[lane + 1];
-        const u32 prev = msk[lane] >> 15;
-        u32 starts = m & ~((m << 1) | prev) & 0xFFFFu;
+        if (ABL == 4) { asm volatile("" ::"v"(m)); return 0; }
+        // neighbours' masks by DPP lane shifts
+        const u32 prevm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x138, 0xF, 0xF, false);   // wave_shr:1
+        const u32 nextm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x130, 0xF, 0xF, false);   // wave_shl:1
+        const bool owner = lane >= 1 && lane <= MAP_OWN;
+        u32 starts = owner ? (m & ~((m << 1) | (prevm >> 15)) & 0xFFFFu) : 0u;
+        const u32 w32 = m | (nextm << 16);
         const u32 cnt = __popc(starts);
         u32 o = 0, total = 0;
 #pragma unroll
@@ -251,89 +342,122 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             o += __builtin_amdgcn_mbcnt_hi((u32)(bal >> 32), __builtin_amdgcn_mbcnt_lo((u32)bal, 0u)) << b;
             total += (u32)__popcll(bal) << b;
         }
+        total = __builtin_amdgcn_readfirstlane(total);
         while (starts) {
-            const int b = __ffs(starts) - 1;
+            const u32 b = __builtin_ctz(starts);
             starts &= starts - 1;
-            sst[o++] = (uint16_t)(16 * lane + b);               // step-relative offset
+            const u32 run = __builtin_ctz(~(w32 >> b));        // >= 1; 32 - b when the window is all letters
+            const u32 len = run < 16 ? run : 16u;              // 16 = long token (> 15 bytes)
+            sst[o++] = (uint16_t)((16 * lane + b) | (len << SST_LEN_SHIFT));
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_lds_sync();
         my_tokens += total;
 
-        // ---- tokens, one per lane per iteration (two per lane with both probes in flight was
-        //      measured slower: ~177 tokens per step fill 3 x 64 slots but 2 x 128)
+        // ---- tokens: uniform iterations of 64 tokens (every lane runs every iteration; lanes
+        //      past `total` are inactive by flag), software-pipelined so that one LDS round trip
+        //      per iteration carries this token's table probe, the next token's key bytes and
+        //      the entry after that; a miss reserves its units here and the wave stores them in
+        //      the next iteration (2 unit stores per iteration + 2 after the loop, see the
+        //      prefetch accounting)
         u32 sink = 0;
-        auto token_key = [&](int off, int& len, u64& k0, u64& k1) {
-            const int rp = MAP_PRE + off;                       // region position
-            const int wi = rp >> 4, bi = rp & 15;
-            const u32 w32 = (u32)msk[wi] | ((u32)msk[wi + 1] << 16);
-            const u32 v = ~(w32 >> bi);                         // >= 17 valid bits
-            len = v ? __ffs(v) - 1 : 32;                        // v == 0: run covers the window
-            // key bytes [rp, rp+16) from LDS via 5 aligned dwords
-            const int al = rp & ~3, sh = rp & 3;
-            const u32* d = reinterpret_cast<const u32*>(bytes + al);
-            const u32 d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
-            const u32 o0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-            const u32 o1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-            const u32 o2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-            const u32 o3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-            const int kl = len < 16 ? len : 15;
-            const u64 b0 = ((u64)o1 << 32 | o0) & low_bytes_mask(kl);
-            const u64 b1 = kl > 8 ? (((u64)o3 << 32 | o2) & low_bytes_mask(kl - 8)) : 0ull;
-            make_key(b0, b1, kl, k0, k1);
-        };
-        for (u32 i = lane; i < total; i += 64) {
-            if (ABL == 1) { sink += sst[i]; continue; }
-            const int off = sst[i];
-            int len;
-            u64 k0, k1;
-            token_key(off, len, k0, k1);
-            if (len >= 16) { my_long++; long_token(a, (u64)(base + off)); continue; }
-            const u32 h = lds_hash(k0, k1);
-            if (ABL == 2) { sink += h; continue; }
-            const bool hit = tab.add(k0, k1, h);
-            if (ABL == 3) { sink += hit; continue; }
+        const u32 iters = (total + 63) >> 6;
+        Tok cur = decode_tok(sst[lane], lane < total, keyread(sst[lane]));
+        u32 e_nxt = sst[64 + lane];
+        u32 o0p = OOB, o1p = OOB;             // pending miss units (previous iteration)
+        u64 k0p = 0, k1p = 0;
+        for (u32 it = 0; it < iters; it++) {
+            if (ABL == 1) { sink += cur.e; cur.e = sst[(it + 1) * 64 + lane]; continue; }
+            if (cur.lng) { my_long++; long_token(a, (u64)(wbase + (cur.e & ((1u << SST_LEN_SHIFT) - 1)))); }
+            const bool med = !cur.shrt;
+            const u64 k0 = (u64)cur.k0h << 32 | cur.k0l, k1 = (u64)cur.k1h << 32 | cur.k1l;
+            if (ABL == 2) { sink += cur.h; cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, keyread(e_nxt));
+                            e_nxt = sst[(it + 2) * 64 + lane]; continue; }
+            // issue together: this token's probe, the next token's key bytes, the entry after
+            const auto pr = tab.probe(med, cur.h);
+            const KeyWords nkw = keyread(e_nxt);
+            const u32 e_nn = sst[(it + 2) * 64 + lane];
+            const bool hit = tab.finish(cur.valid, med, k0, k1, pr);
+            if (ABL == 3) { sink += hit; cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, nkw); e_nxt = e_nn; continue; }
             my_hits += (u32)hit;
-            if (!hit) miss(k0, k1, h);
+            // miss: reserve units in the (workgroup, bucket) region
+            const u32 p = miss_bucket(cur.h, a.pmask);
+            const u32 nu = cur.shrt ? 1u : 2u;
+            u32 pos = 0xFFFFFFFFu;
+            const bool miss = cur.valid && !hit;
+            if (miss) pos = atomicAdd(&cursor[p], nu);
+            // the previous iteration's miss units
+            unit_store(prsrc, o0p, k0p);
+            unit_store(prsrc, o1p, k1p);
+            const bool was_short = cur.shrt;
+            cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, nkw);
+            e_nxt = e_nn;
+            o0p = OOB; o1p = OOB; k0p = k0; k1p = k1;
+            if (miss) {
+                if (pos + nu <= a.region_cap) {
+                    o0p = (u32)((p * a.region_cap + pos) * 8);
+                    o1p = was_short ? OOB : o0p + 8;
+                } else {                                        // region full: zero its tail, global table
+                    u64* r = wpool + (u64)p * a.region_cap;
+                    for (u32 k = pos; k < a.region_cap; k++) r[k] = 0;
+                    my_global++;
+                    ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
+                }
+            }
+        }
+        if (ABL == 0) {
+            unit_store(prsrc, o0p, k0p);
+            unit_store(prsrc, o1p, k1p);
         }
         if (ABL) asm volatile("" ::"v"(sink));
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_lds_sync();
+        return (ABL == 0) ? iters + 1 : 0u;
     };
 
-    // two steps in flight per wave (A/B register sets, no copies between them).  A wave's
-    // steps increase, so once one reaches past the input end (a "tail" step) all later ones do:
-    // the main loop stops there and the tail steps are reloaded byte-exactly after it (keeping
-    // the cold reload path's registers out of the loop)
-    auto is_tail = [&](u64 step) { return step * MAP_STEP + MAP_STEP + MAP_LOOK > a.n; };
+    // ---- main loop, unrolled over the register sets so that each set's load and waits name
+    //      fixed registers (tools/check_inflight.py); a set's load was issued MAP_SETS steps
+    //      earlier; h1..h3 = unit-store pairs of the last three steps (the wait count)
+    auto is_tail = [&](u64 step) { return step * MAP_STEP - 16 + MAP_WIN > a.n; };
     auto u4 = [](v4u v) { return make_uint4(v.x, v.y, v.z, v.w); };
-    v4u ma, xa, mb, xb;
+    v4u mA, mB, mC, mD;
     u64 st = (u64)blockIdx.x * MAP_WAVES + wave;
-    const std::integral_constant<int, 0> SA;
-    const std::integral_constant<int, 1> SB;
-    load(SA, st, ma, xa);
-    load(SB, st + stride, mb, xb);
-    while (st < nsteps && !is_tail(st)) {
-        buf_wait_A<2>(ma, xa);                   // younger: B's two loads
-        process(st, u4(ma), u4(xa));
-        load(SA, st + 2 * stride, ma, xa);
-        st += stride;
-        if (st >= nsteps || is_tail(st)) break;
-        buf_wait_B<2>(mb, xb);                   // younger: A's two loads
-        process(st, u4(mb), u4(xb));
-        load(SB, st + 2 * stride, mb, xb);
-        st += stride;
+    {
+        v4i r; u32 om;
+        addr(st, r, om);              set_load_A(r, om, mA);
+        addr(st + stride, r, om);     set_load_B(r, om, mB);
+        if (MAP_SETS == 4) {
+            addr(st + 2 * stride, r, om); set_load_C(r, om, mC);
+            addr(st + 3 * stride, r, om); set_load_D(r, om, mD);
+        }
     }
-    buf_wait_A<0>(ma, xa);                       // nothing may land in a dead register
-    buf_wait_B<0>(mb, xb);
-    for (; st < nsteps; st += stride) {
-        const long org = (long)(st * MAP_STEP) - MAP_PRE;
-        const uint4 mine = load_chunk(a.in, a.n, org + 16 * (lane + 1));
-        const uint4 extra = xc >= 0 ? load_chunk(a.in, a.n, org + 16 * xc) : make_uint4(0, 0, 0, 0);
-        process(st, mine, extra);
+    u32 h1 = 0, h2 = 0, h3 = 0;
+#define WCG_MAP_STEP(S)                                                                         \
+    {                                                                                           \
+        if (st >= nsteps || is_tail(st)) break;                                                 \
+        v4i r; u32 om;                                                                          \
+        addr(st + MAP_SETS * stride, r, om);                                                    \
+        set_wait_##S((MAP_SETS - 1) + 2 * (h1 + (MAP_SETS == 4 ? h2 + h3 : 0)), m##S);          \
+        const u32 it_ = process(st, u4(m##S));                                                  \
+        set_load_##S(r, om, m##S);                                                              \
+        h3 = h2; h2 = h1; h1 = it_;                                                             \
+        st += stride;                                                                           \
     }
+    while (true) {
+        WCG_MAP_STEP(A)
+        WCG_MAP_STEP(B)
+#if WCG_MAP_SETS == 4
+        WCG_MAP_STEP(C)
+        WCG_MAP_STEP(D)
+#endif
+    }
+#undef WCG_MAP_STEP
+    set_wait_n_A<0>(mA);                  // nothing may land in a dead register
+    set_wait_n_B<0>(mB);
+    if (MAP_SETS == 4) {
+        set_wait_n_C<0>(mC);
+        set_wait_n_D<0>(mD);
+    }
+    for (; st < nsteps; st += stride)     // tail steps: byte-exact reloads
+        process(st, load_chunk(a.in, a.n, (long)(st * MAP_STEP) - 16 + 16 * lane));
 
     // ---- flush the LDS table into this workgroup's miss-log regions (entries with counts);
     //      a full region -> global table
@@ -352,16 +476,22 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         const u32 c = cursor[p];
         a.region_len[(u64)blockIdx.x * (a.pmask + 1) + p] = c < a.region_cap ? c : (u32)a.region_cap;
     }
-    // stats: one atomic per wave
+    // stats: per-workgroup partial sums with plain stores (k_agg's first workgroup adds them
+    // to DevState).  Per-wave atomics on DevState cost ~12 ns each serialised on one line:
+    // 16K of them added 0.2 ms to every launch.
+    __shared__ u64 wsum[MAP_WAVES][4];
     u64 v0 = lane == 0 ? my_tokens : 0, v1 = my_hits, v2 = my_global, v3 = my_long;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         v0 += __shfl_xor(v0, d, 64); v1 += __shfl_xor(v1, d, 64);
         v2 += __shfl_xor(v2, d, 64); v3 += __shfl_xor(v3, d, 64);
     }
-    if (lane == 0) {
-        atomicAdd(&a.st->tokens, v0); atomicAdd(&a.st->lds_hits, v1);
-        atomicAdd(&a.st->global_ops, v2); atomicAdd(&a.st->long_tokens, v3);
+    if (lane == 0) { wsum[wave][0] = v0; wsum[wave][1] = v1; wsum[wave][2] = v2; wsum[wave][3] = v3; }
+    __syncthreads();
+    if (tid < 4) {
+        u64 t = 0;
+        for (int w = 0; w < MAP_WAVES; w++) t += wsum[w][tid];
+        a.wg_stats[(u64)blockIdx.x * 4 + tid] = t;
     }
 }
 

@@ -10,7 +10,8 @@ import os
 from typing import List, Optional, Tuple
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwcg.so")
+# WCG_LIB: an alternative build of the same library (measurement variants only)
+LIB_PATH = os.environ.get("WCG_LIB") or os.path.join(_HERE, "libwcg.so")
 
 WCG_OK, WCG_EINVAL, WCG_ENOMEM, WCG_EHIP, WCG_EFULL, WCG_ESTATE = range(6)
 RECORD_BYTES = 32

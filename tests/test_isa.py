@@ -36,7 +36,18 @@ def device_asm(tmp_path_factory):
 def test_map_asm_loads_not_copied_before_wait(device_asm):
     errors, loads, waits = check_inflight.check(device_asm, KMAP0)
     assert not errors, errors
-    assert set(loads) == {"A0", "A1", "B0", "B1"} and len(waits) == 4
+    sets = "ABCD"
+    assert set(loads) == {s + "0" for s in sets}
+    # every set: a counted wait in each unrolled step and the drain after the loop
+    assert sorted({w[0] for w in waits}) == list(sets) and len(waits) >= 2 * len(sets)
+
+
+def test_map_unit_stores_unconditional(device_asm):
+    """The prefetch accounting counts 2 miss-log unit stores per token iteration: they must be
+    the inline-asm stores, at least two per inlined copy of the step."""
+    lines = check_inflight.kernel_lines(device_asm, KMAP0)
+    stores = [l for l in lines if "wcg-store" in l]
+    assert stores and all("buffer_store_dwordx2" in l for l in stores) and len(stores) % 2 == 0
 
 
 def test_map_no_scratch(device_asm):

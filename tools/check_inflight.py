@@ -10,9 +10,12 @@ in an assembly comment:
     buffer_load_dwordx4 v[14:17], v4, s[12:15], 0 offen ; wcg-load A0
     s_waitcnt vmcnt(2) ; wcg-wait A v[14:17] v[6:9]
 
+(a quantised wait is one asm statement - a chain of scalar compares around several s_waitcnt -
+whose last line carries the tag; the tag names the registers the whole statement holds)
+
 A value can only move to a different register through a copy, so requiring that every load of a
 tag writes the same registers, and that every wait of a set names exactly those registers
-(A0/A1 for set A, B0/B1 for set B), rules such copies out without any control-flow analysis.
+(A0/A1 for set A, B0/B1 for set B, ...), rules such copies out without any control-flow analysis.
 
 Usage: check_inflight.py FILE.s KERNEL_SYMBOL      (exit status 1 on a violation)
 """
@@ -34,16 +37,17 @@ def check(text, sym):
         if m:
             loads.setdefault(m.group(2), set()).add(m.group(1))
             continue
-        m = re.search(r"s_waitcnt\s+vmcnt\(\d+\).*wcg-wait\s+(\w)\s+(v\[\d+:\d+\])\s+(v\[\d+:\d+\])", ln)
+        m = re.search(r"wcg-wait\s+(\w)((?:\s+v\[\d+:\d+\])+)", ln)
         if m:
-            waits.append((m.group(1), m.group(2), m.group(3)))
+            waits.append((m.group(1),) + tuple(m.group(2).split()))
     if not loads or not waits:
         errors.append("no tagged loads/waits found (kernel not built from wcg_map.h?)")
     for tag, regs in sorted(loads.items()):
         if len(regs) != 1:
             errors.append(f"loads tagged {tag} write different registers: {sorted(regs)}")
-    for s, r0, r1 in waits:
-        for tag, r in ((s + "0", r0), (s + "1", r1)):
+    for w in waits:
+        s = w[0]
+        for tag, r in ((s + str(i), r) for i, r in enumerate(w[1:])):
             if loads.get(tag) != {r}:
                 errors.append(f"wait of set {s} names {r}, loads tagged {tag} write {sorted(loads.get(tag, []))}")
     return sorted(set(errors)), loads, waits
