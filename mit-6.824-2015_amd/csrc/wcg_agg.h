@@ -14,7 +14,8 @@ namespace wcg {
 
 constexpr int AGG_NT = 1024;
 constexpr u32 AGG_BATCH = AGG_NT * 4;     // units per batch (4 per thread)
-constexpr int AGG_NB = 1690;           // 1690 x 4 slots x 24 B (u64 counts) = 162240 B (+ 1.5 KiB)
+constexpr int AGG_W = 2;               // ways per bucket (16-byte k0 rows: wcg_lds_table.h)
+constexpr int AGG_NB = 3380;           // 3380 x 2 slots x 24 B (u64 counts) = 162240 B (+ 1.5 KiB)
 constexpr u32 AGG_MAX_SRC = 256;       // source regions per workgroup (+1 KiB LDS = 160 KiB)
 
 struct AggArgs {
@@ -31,12 +32,12 @@ struct AggArgs {
 };
 
 __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
-    __shared__ __align__(16) u64 tk0[AGG_NB][4];
-    __shared__ __align__(16) u64 tk1[AGG_NB][4];
-    __shared__ u64 tcnt[AGG_NB][4];
+    __shared__ __align__(16) u64 tk0[AGG_NB][AGG_W];
+    __shared__ __align__(16) u64 tk1[AGG_NB][AGG_W];
+    __shared__ u64 tcnt[AGG_NB][AGG_W];
     __shared__ u32 rlen_s[AGG_MAX_SRC];
     const int tid = threadIdx.x;
-    LdsTable<AGG_NB, u64> tab{tk0, tk1, tcnt};
+    LdsTable<AGG_NB, u64, AGG_W> tab{tk0, tk1, tcnt};
     tab.init(tid, AGG_NT);
     const u32 p = blockIdx.x % a.P, s = blockIdx.x / a.P;
     const u32 w0 = (u32)(((u64)a.nsrc * s) / a.slices), w1 = (u32)(((u64)a.nsrc * (s + 1)) / a.slices);
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
         load(wb, bb, b0, b1, b2);
     }
     __syncthreads();
-    for (int i = tid; i < AGG_NB * 4; i += AGG_NT) {
+    for (int i = tid; i < AGG_NB * AGG_W; i += AGG_NT) {
         const u64 c = (&tcnt[0][0])[i];
         if (!c) continue;
         const u64 k0 = (&tk0[0][0])[i], k1 = (&tk1[0][0])[i];

@@ -305,7 +305,9 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // the global table
     const u32 P = c->nbuckets;
     u64 per_wg_bytes = (u64)a.tiles_per_wg * MAP_STEP;
-    a.region_cap = std::max<u64>(2048, per_wg_bytes / (8ull * P)) & ~1ull;   // even: 16-byte aligned regions
+    // even (16-byte aligned regions); a workgroup's regions stay under 2 GiB so k_map's unit
+    // offsets fit 32 bits and its 24-bit multiplies (P * region_cap * 8 <= 2^31)
+    a.region_cap = std::min<u64>(std::max<u64>(2048, per_wg_bytes / (8ull * P)), (1ull << 31) / (8ull * P)) & ~1ull;
     a.pmask = P - 1;
     u64 need = grid * P * a.region_cap * sizeof(u64);
     if (need > c->pool_bytes) {
@@ -439,15 +441,15 @@ int wcg_partition(wcg_ctx* c, uint32_t nreduce, uint32_t r, uint8_t* host_out, u
 }
 
 int wcg_export(wcg_ctx* c, uint32_t nreduce, uint32_t nranks, const void** dev_records, uint64_t* counts) {
-    if (!c || !counts || nreduce == 0 || nranks == 0 || nranks > 1024) return WCG_EINVAL;
+    if (!c || !counts || nreduce == 0 || nranks == 0 || nranks > EX_MAX_RANKS) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
     if ((rc = compact(c))) return rc;
     u64 n = c->nrec;
     HIPCHK(c, hipMemsetAsync(c->d_per_rank, 0, 2 * 1024 * sizeof(u64), c->stream));
     if (n) {
-        k_export_count<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recA, n, nreduce, nranks, c->arena,
-                                                                             c->owner, c->d_per_rank);
+        k_export_count<<<(unsigned)((n + EX_TILE - 1) / EX_TILE), EX_NT, 0, c->stream>>>(c->recA, n, nreduce, nranks,
+                                                                                        c->arena, c->owner, c->d_per_rank);
         HIPCHK(c, hipGetLastError());
     }
     std::vector<u64> per(nranks), cur(nranks);
@@ -459,8 +461,8 @@ int wcg_export(wcg_ctx* c, uint32_t nreduce, uint32_t nranks, const void** dev_r
     if (rc) return rc;
     if (n) {
         HIPCHK(c, hipMemcpyAsync(c->d_per_rank + 1024, cur.data(), nranks * sizeof(u64), hipMemcpyHostToDevice, c->stream));
-        k_export_write<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recA, n, c->owner, c->d_per_rank + 1024,
-                                                                             c->arena, c->exp_buf);
+        k_export_write<<<(unsigned)((n + EX_TILE - 1) / EX_TILE), EX_NT, 0, c->stream>>>(
+            c->recA, n, nranks, c->owner, c->d_per_rank + 1024, c->arena, c->exp_buf);
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -225,30 +225,11 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 // copied, and N counts only this wave's own younger asm loads (compiler-issued memory ops in
 // between can only make a wait stronger).
 //
-// Each load and wait carries a tag in an assembly comment ("wcg-load A0", "wcg-wait A v[..]
-// v[..]") naming its register set.  tools/check_inflight.py requires every tagged load and wait
-// of a set to use the same physical registers: a register copy between an asm load and its wait
-// (which would read data that has not landed) cannot pass that check (tests/test_isa.py).
-#define WCG_TAG_LOAD(TAG)                                                                      \
-    __device__ __forceinline__ v4u buf_load16_##TAG(v4i rsrc, u32 off) {                      \
-        v4u r;                                                                                 \
-        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen ; wcg-load " #TAG                \
-                     : "=&v"(r) : "v"(off), "s"(rsrc) : "memory");                             \
-        return r;                                                                              \
-    }
-WCG_TAG_LOAD(A0)
-WCG_TAG_LOAD(A1)
-WCG_TAG_LOAD(B0)
-WCG_TAG_LOAD(B1)
-#undef WCG_TAG_LOAD
-template <int N>
-__device__ __forceinline__ void buf_wait_A(v4u& x, v4u& y) {
-    asm volatile("s_waitcnt vmcnt(%2) ; wcg-wait A %0 %1" : "+v"(x), "+v"(y) : "n"(N) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void buf_wait_B(v4u& x, v4u& y) {
-    asm volatile("s_waitcnt vmcnt(%2) ; wcg-wait B %0 %1" : "+v"(x), "+v"(y) : "n"(N) : "memory");
-}
+// Each load and wait carries a tag in an assembly comment ("wcg-load A0", "wcg-wait A v[..]")
+// naming its register set (the set ops are in wcg_map.h).  tools/check_inflight.py requires
+// every tagged load and wait of a set to use the same physical registers: a register copy
+// between an asm load and its wait (which would read data that has not landed) cannot pass that
+// check (tests/test_isa.py).
 __device__ __forceinline__ v4i make_rsrc(const void* base, u32 nbytes) {
     const u64 p = (u64)base;
     v4i r;

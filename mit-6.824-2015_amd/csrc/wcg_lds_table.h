@@ -1,33 +1,37 @@
-// wcg_lds_table.h - exact-key hash table in LDS (one per workgroup), 2-choice x 4-way buckets.
+// wcg_lds_table.h - exact-key hash tables in LDS (one per workgroup).
 //
-// Keys are the fixed-width identities of fact F4 (k0 = bytes 0-7 [| len << 56 for len <= 7],
-// k1 = bytes 8-14 | len << 56 or 0).  A key may live in 8 slots: 4 in bucket b1 and 4 in
-// bucket b2.  A probe reads both buckets' k0 words (4 x ds_read_b128, independent), so a lookup
-// costs ONE LDS round trip; the measured alternatives (tag bytes first, or bucket b1 before b2)
-// add a dependent round trip and were slower.  The probe is split into start()
-// (issue the reads) and finish() (match / insert) so a lane can keep two lookups in flight.
-// Insertion claims an empty slot with a 64-bit LDS CAS on k0 and then publishes k1.  Two lanes
-// inserting the same new key at the same moment can end up in two different slots: that
-// duplicate is harmless (both counts are flushed and summed downstream), so no lane ever waits
-// for another lane's publish.
+// LdsTable (k_agg): 2-choice x W-way buckets.  Keys are the fixed-width identities of fact F4
+// (k0 = bytes 0-7 [| len << 56 for len <= 7], k1 = bytes 8-14 | len << 56 or 0).  A key may
+// live in 2W slots: W in bucket b1 and W in bucket b2.  A probe reads both buckets' k0 rows
+// (independent ds_read_b128s), so a lookup costs ONE LDS round trip; the measured alternatives
+// (tag bytes first, or bucket b1 before b2) add a dependent round trip and were slower.  Rows
+// are W x 8 bytes: random 16-byte rows (W = 2) start on 16 distinct bank quads, 32-byte rows on
+// only 8, and a 16-lane ds_read_b128 group of random rows conflicts less the more quads it can
+// spread over (k_agg measured 74% of its LDS cycles in bank conflicts with W = 4).  The probe is
+// split into start() (issue the reads) and finish() (match / insert) so a lane can keep two
+// lookups in flight.  Insertion claims an empty slot with a 64-bit LDS CAS on k0 and then
+// publishes k1.  Two lanes inserting the same new key at the same moment can end up in two
+// different slots: that duplicate is harmless (both counts are flushed and summed downstream),
+// so no lane ever waits for another lane's publish.
 #pragma once
 #include "wcg_common.h"
 
 namespace wcg {
 
-template <int NB, typename CNT>
+template <int NB, typename CNT, int W>
 struct LdsTable {
-    u64 (*k0)[4];      // [NB][4]  (32-byte rows)
-    u64 (*k1)[4];      // [NB][4]
-    CNT (*cnt)[4];     // [NB][4]
+    static_assert(W == 2 || W == 4, "rows of one or two 16-byte reads");
+    u64 (*k0)[W];      // [NB][W]  (W x 8-byte rows)
+    u64 (*k1)[W];      // [NB][W]
+    CNT (*cnt)[W];     // [NB][W]
 
     struct Probe {
         u32 b1, b2;
-        u64 v[4], w[4];
+        u64 v[W], w[W];
     };
 
     __device__ __forceinline__ void init(int tid, int nt) {
-        for (int i = tid; i < NB * 4; i += nt) {
+        for (int i = tid; i < NB * W; i += nt) {
             (&k0[0][0])[i] = 0;
             (&k1[0][0])[i] = 0;
             (&cnt[0][0])[i] = 0;
@@ -40,32 +44,36 @@ struct LdsTable {
         if (b2 == b1) b2 = (b1 + 1 == (u32)NB) ? 0 : b1 + 1;
     }
 
-    __device__ __forceinline__ void read4(u32 b, u64 (&v)[4]) const {
+    __device__ __forceinline__ void readrow(u32 b, u64 (&v)[W]) const {
         const uint4* p = reinterpret_cast<const uint4*>(&k0[b][0]);
-        const uint4 x = p[0], y = p[1];
-        v[0] = (u64)x.y << 32 | x.x; v[1] = (u64)x.w << 32 | x.z;
-        v[2] = (u64)y.y << 32 | y.x; v[3] = (u64)y.w << 32 | y.z;
+#pragma unroll
+        for (int q = 0; q < W / 2; q++) {
+            const uint4 x = p[q];
+            v[2 * q] = (u64)x.y << 32 | x.x;
+            v[2 * q + 1] = (u64)x.w << 32 | x.z;
+        }
     }
 
     __device__ __forceinline__ void start(u32 h, Probe& p) const {
         buckets(h, p.b1, p.b2);
-        read4(p.b1, p.v);
-        read4(p.b2, p.w);
+        readrow(p.b1, p.v);
+        readrow(p.b2, p.w);
     }
 
     __device__ __forceinline__ void add_cnt(u32 b, int j, CNT c) { atomicAdd(&cnt[b][j], c); }
 
-    // match (slot s: bucket s >> 2, way s & 3) or insert; false when both buckets are full of
-    // other keys.  Straight-line common path: bit masks and one atomic at a computed address.
+    // match (slot s: bucket b1 for s < W, else b2; way s % W) or insert; false when both
+    // buckets are full of other keys.  Straight-line common path: bit masks and one atomic at a
+    // computed address.
     __device__ __forceinline__ bool finish(u64 a0, u64 a1, const Probe& p, CNT c) {
         const bool shrt = key_short(a0);
         u32 m = 0, e = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < W; j++) {
             m |= (u32)(p.v[j] == a0) << j;
-            m |= (u32)(p.w[j] == a0) << (4 + j);
+            m |= (u32)(p.w[j] == a0) << (W + j);
             e |= (u32)(p.v[j] == 0) << j;
-            e |= (u32)(p.w[j] == 0) << (4 + j);
+            e |= (u32)(p.w[j] == 0) << (W + j);
         }
         if (!shrt && m) {                       // keys of 8+ bytes: confirm k1 (usually 1 candidate)
             u32 mm = m;
@@ -73,19 +81,19 @@ struct LdsTable {
             while (mm) {
                 const int s = __ffs(mm) - 1;
                 mm &= mm - 1;
-                if (k1[s < 4 ? p.b1 : p.b2][s & 3] == a1) { m = 1u << s; break; }
+                if (k1[s < W ? p.b1 : p.b2][s % W] == a1) { m = 1u << s; break; }
             }
         }
         if (m) {
             const int s = __ffs(m) - 1;
-            add_cnt(s < 4 ? p.b1 : p.b2, s & 3, c);
+            add_cnt(s < W ? p.b1 : p.b2, s % W, c);
             return true;
         }
         while (e) {                             // insert: first empty slot of b1, then b2
             const int s = __ffs(e) - 1;
             e &= e - 1;
-            const u32 b = s < 4 ? p.b1 : p.b2;
-            const int j = s & 3;
+            const u32 b = s < W ? p.b1 : p.b2;
+            const int j = s % W;
             const u64 old = atomicCAS(&k0[b][j], 0ull, a0);
             if (old == 0) {
                 if (!shrt) k1[b][j] = a1;
@@ -109,9 +117,8 @@ struct LdsTable {
 // the C2 corpus (and a simulation of the same stream): associativity hardly moves the hit rate
 // (2-choice x 1-way 0.678 vs 2-choice x 4-way 0.693 at equal slots) but capacity does, and
 // short keys need 40% less room without a k1 word.  A probe is 2 slots x (k0, k1) loads and
-// compares, the same instructions for both kinds (the table bases are selected per lane; a
-// short key's k1 "slot" is a shared zero word), because k_map is VALU-issue bound and a
-// divergent second probe would cost every wave both.
+// compares, the same instructions for both kinds (the table bases are selected per lane; the
+// short keys' k1 is a shared zero word), so a wave never runs two probe paths.
 template <int NS, int NM>
 struct MapTable {
     u64* sk0;      // [NS]
@@ -143,9 +150,12 @@ struct MapTable {
         Probe p;
         slots(h, med ? (u32)NM : (u32)NS, p.s1, p.s2);
         const u64* K0 = med ? mk0 : sk0;
+        p.x1 = K0[p.s1]; p.x2 = K0[p.s2];
+        // a short key's k1 "slot" is a shared zero word (a broadcast read): no branch (the
+        // exec-masked form, reads for medium lanes only, measured no faster)
         const u64* K1a = med ? mk1 + p.s1 : zero;
         const u64* K1b = med ? mk1 + p.s2 : zero;
-        p.x1 = K0[p.s1]; p.x2 = K0[p.s2]; p.y1 = *K1a; p.y2 = *K1b;
+        p.y1 = *K1a; p.y2 = *K1b;
         return p;
     }
     __device__ __forceinline__ bool finish(bool valid, bool med, u64 a0, u64 a1, const Probe& p) {
@@ -153,7 +163,7 @@ struct MapTable {
         u32* C = med ? mcnt : scnt;
         const bool h1 = p.x1 == a0 && p.y1 == a1, h2 = p.x2 == a0 && p.y2 == a1;
         const bool hit = valid && (h1 || h2);
-        if (hit) atomicAdd(&C[h1 ? p.s1 : p.s2], 1u);
+        atomicAdd(&C[h1 ? p.s1 : p.s2], hit ? 1u : 0u);     // every lane (0 = no hit): no branch
         if (!valid || hit || (p.x1 != 0 && p.x2 != 0)) return hit;
         // insert: claim an empty slot's k0, then publish k1 (a reader that sees k0 before k1
         // treats the slot as another key and may insert a duplicate: harmless, both counts are

@@ -14,7 +14,7 @@
 //      DPP lane shifts; each start's run length is read off the 32-bit mask window (own | next);
 //      the wave compacts {offset, length} entries (prefix sum from 4 ballots + mbcnt) into its
 //      LDS list;
-//   4. tokens, 64 per uniform iteration: key identity (<= 15 bytes, fact F4) from two unaligned
+//   4. tokens, 64 per uniform iteration: key identity (<= 15 bytes, fact F4) from three aligned
 //      8-byte LDS reads -> the workgroup's LDS tables (exact keys, short and medium keys in
 //      2-choice x 1-slot tables, u32 counts: MapTable); a miss is appended to this workgroup's
 //      region of the miss log for k_agg; tokens > 15 bytes go to the long-key table with an
@@ -27,9 +27,9 @@
 // memory operations are done (loads and stores retire in issue order).  A step's processing
 // issues exactly 2 miss-log stores per token iteration plus 2 after its last one (inline-asm
 // buffer stores executed by the whole wave, out-of-range offsets for lanes without a miss), so
-// when set s is due the number of operations issued after its loads is known: 2 loads +
-// 2 * (iters + 1) for each of the MAP_SETS - 1 steps processed since.  The wait uses the largest quantised N not above that
-// count; any operation the count does not know about (rare paths: long tokens, a full miss-log
+// when set s is due the number of operations issued after its loads is known: the other sets'
+// MAP_SETS - 1 loads + 2 * (iters + 1) for each of the MAP_SETS - 1 steps processed since.  The
+// wait uses the largest quantised N not above that count; any operation the count does not know about (rare paths: long tokens, a full miss-log
 // region, UTF-8 table loads) can only make the wait stronger.
 #pragma once
 #include <type_traits>
@@ -197,7 +197,8 @@ __device__ __forceinline__ void wave_lds_sync() {
     "s_waitcnt vmcnt(0)\n99: ; " TAG
 #define WCG_SET_OPS(S)                                                                          \
     __device__ __forceinline__ void set_load_##S(v4i rsrc, u32 om, v4u& m) {                    \
-        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen ; wcg-load " #S "0"               \
+        /* s_nop 4: the descriptor SGPRs may have just been written by a VALU readfirstlane */    \
+        asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen ; wcg-load " #S "0"    \
                      : "=&v"(m) : "v"(om), "s"(rsrc) : "memory");                               \
     }                                                                                           \
     template <int N>                                                                            \
@@ -356,15 +357,31 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         // ---- tokens: uniform iterations of 64 tokens (every lane runs every iteration; lanes
         //      past `total` are inactive by flag), software-pipelined so that one LDS round trip
         //      per iteration carries this token's table probe, the next token's key bytes and
-        //      the entry after that; a miss reserves its units here and the wave stores them in
-        //      the next iteration (2 unit stores per iteration + 2 after the loop, see the
-        //      prefetch accounting)
+        //      the entry after that.  A miss reserves its units with an LDS atomic whose result
+        //      is read one iteration later (after that iteration's probe reads have returned, so
+        //      the reservation adds no round trip of its own), and the wave stores the units
+        //      then: 2 unit stores per iteration + 2 after the loop (prefetch accounting)
         u32 sink = 0;
         const u32 iters = (total + 63) >> 6;
         Tok cur = decode_tok(sst[lane], lane < total, keyread(sst[lane]));
         u32 e_nxt = sst[64 + lane];
-        u32 o0p = OOB, o1p = OOB;             // pending miss units (previous iteration)
+        bool missp = false;                   // the previous iteration's miss: bucket, units,
+        u32 pp = 0, nup = 0, posp = 0;        // reservation and key
         u64 k0p = 0, k1p = 0;
+        const u32 rcap = (u32)a.region_cap;   // < 2^22 (host), so offsets fit 24-bit multiplies
+        auto store_pending = [&]() {
+            const bool fits = missp && posp + nup <= rcap;
+            const u32 o0 = fits ? (__umul24(pp, rcap) + posp) * 8u : OOB;
+            const u32 o1 = fits && nup == 2 ? o0 + 8u : OOB;
+            unit_store(prsrc, o0, k0p);
+            unit_store(prsrc, o1, k1p);
+            if (missp && !fits) {             // region full: zero its tail, global table
+                u64* r = wpool + (u64)pp * a.region_cap;
+                for (u32 k = posp; k < rcap; k++) r[k] = 0;
+                my_global++;
+                ginsert(a.gtab, a.gmask, k0p, k1p, gslot(key_hash(k0p, k1p)), 1, a.st);
+            }
+        };
         for (u32 it = 0; it < iters; it++) {
             if (ABL == 1) { sink += cur.e; cur.e = sst[(it + 1) * 64 + lane]; continue; }
             if (cur.lng) { my_long++; long_token(a, (u64)(wbase + (cur.e & ((1u << SST_LEN_SHIFT) - 1)))); }
@@ -379,35 +396,17 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             const bool hit = tab.finish(cur.valid, med, k0, k1, pr);
             if (ABL == 3) { sink += hit; cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, nkw); e_nxt = e_nn; continue; }
             my_hits += (u32)hit;
-            // miss: reserve units in the (workgroup, bucket) region
-            const u32 p = miss_bucket(cur.h, a.pmask);
-            const u32 nu = cur.shrt ? 1u : 2u;
-            u32 pos = 0xFFFFFFFFu;
-            const bool miss = cur.valid && !hit;
-            if (miss) pos = atomicAdd(&cursor[p], nu);
-            // the previous iteration's miss units
-            unit_store(prsrc, o0p, k0p);
-            unit_store(prsrc, o1p, k1p);
-            const bool was_short = cur.shrt;
+            store_pending();                  // the previous iteration's miss units
+            // this token's miss: reserve units in the (workgroup, bucket) region
+            missp = cur.valid && !hit;
+            pp = miss_bucket(cur.h, a.pmask);
+            nup = cur.shrt ? 1u : 2u;
+            posp = atomicAdd(&cursor[pp], missp ? nup : 0u);   // every lane (0 = no miss)
+            k0p = k0; k1p = k1;
             cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, nkw);
             e_nxt = e_nn;
-            o0p = OOB; o1p = OOB; k0p = k0; k1p = k1;
-            if (miss) {
-                if (pos + nu <= a.region_cap) {
-                    o0p = (u32)((p * a.region_cap + pos) * 8);
-                    o1p = was_short ? OOB : o0p + 8;
-                } else {                                        // region full: zero its tail, global table
-                    u64* r = wpool + (u64)p * a.region_cap;
-                    for (u32 k = pos; k < a.region_cap; k++) r[k] = 0;
-                    my_global++;
-                    ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
-                }
-            }
         }
-        if (ABL == 0) {
-            unit_store(prsrc, o0p, k0p);
-            unit_store(prsrc, o1p, k1p);
-        }
+        if (ABL == 0) store_pending();
         if (ABL) asm volatile("" ::"v"(sink));
         wave_lds_sync();
         return (ABL == 0) ? iters + 1 : 0u;

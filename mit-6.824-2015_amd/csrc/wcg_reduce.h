@@ -367,23 +367,60 @@ __device__ __forceinline__ u64 rec_units(const Rec& r) {
     return (r.ref & LONG_FLAG) ? 1 + ((rec_len(r) + CONT_BYTES - 1) / CONT_BYTES) : 1;
 }
 
-__global__ void k_export_count(const Rec* r, u64 n, u32 nreduce, u32 nranks, const uint8_t* arena, u32* owner,
-                               u64* per_rank) {
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        Rec x = r[i];
-        u32 o = (rec_ihash(x, arena) % nreduce) % nranks;
-        owner[i] = o;
-        atomicAdd(&per_rank[o], rec_units(x));
+// Both export kernels take EX_TILE records per workgroup and count units per owner in LDS, so
+// global atomics are one per (workgroup, owner): with one atomic per record, all records of an
+// owner serialise on one address (~12 ns each: 1.2 ms for 1e5 records to one owner).
+constexpr int EX_NT = 256, EX_IPT = 8, EX_TILE = EX_NT * EX_IPT;
+constexpr u32 EX_MAX_RANKS = 1024;
+
+__global__ __launch_bounds__(EX_NT) void k_export_count(const Rec* r, u64 n, u32 nreduce, u32 nranks,
+                                                        const uint8_t* arena, u32* owner, u64* per_rank) {
+    __shared__ u32 units[EX_MAX_RANKS];
+    for (u32 o = threadIdx.x; o < nranks; o += EX_NT) units[o] = 0;
+    __syncthreads();
+    const u64 base = (u64)blockIdx.x * EX_TILE;
+#pragma unroll
+    for (int k = 0; k < EX_IPT; k++) {
+        const u64 i = base + k * EX_NT + threadIdx.x;
+        if (i < n) {
+            const Rec x = r[i];
+            const u32 o = (rec_ihash(x, arena) % nreduce) % nranks;
+            owner[i] = o;
+            atomicAdd(&units[o], (u32)rec_units(x));
+        }
     }
+    __syncthreads();
+    for (u32 o = threadIdx.x; o < nranks; o += EX_NT)
+        if (units[o]) atomicAdd(&per_rank[o], (u64)units[o]);
 }
 
-// cursor[o] starts at the exclusive prefix of per_rank; order inside a destination is
-// irrelevant (the receiver re-aggregates and re-sorts).
-__global__ void k_export_write(const Rec* r, u64 n, const u32* owner, u64* cursor, const uint8_t* arena, Rec* out) {
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        Rec x = r[i];
-        u64 u = rec_units(x);
-        u64 pos = atomicAdd(&cursor[owner[i]], u);
+// cursor[o] starts at the exclusive prefix of per_rank; a workgroup reserves one range per owner
+// and places its records inside it by LDS atomics.  Order inside a destination is irrelevant
+// (the receiver re-aggregates and re-sorts).
+__global__ __launch_bounds__(EX_NT) void k_export_write(const Rec* r, u64 n, u32 nranks, const u32* owner,
+                                                        u64* cursor, const uint8_t* arena, Rec* out) {
+    __shared__ u32 units[EX_MAX_RANKS];
+    __shared__ u64 first[EX_MAX_RANKS];
+    for (u32 o = threadIdx.x; o < nranks; o += EX_NT) units[o] = 0;
+    __syncthreads();
+    const u64 base = (u64)blockIdx.x * EX_TILE;
+    u32 local[EX_IPT];
+#pragma unroll
+    for (int k = 0; k < EX_IPT; k++) {
+        const u64 i = base + k * EX_NT + threadIdx.x;
+        local[k] = i < n ? atomicAdd(&units[owner[i]], (u32)rec_units(r[i])) : 0u;
+    }
+    __syncthreads();
+    for (u32 o = threadIdx.x; o < nranks; o += EX_NT)
+        first[o] = units[o] ? atomicAdd(&cursor[o], (u64)units[o]) : 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < EX_IPT; k++) {
+        const u64 i = base + k * EX_NT + threadIdx.x;
+        if (i >= n) continue;
+        const Rec x = r[i];
+        const u64 u = rec_units(x);
+        const u64 pos = first[owner[i]] + local[k];
         if (!(x.ref & LONG_FLAG)) { out[pos] = x; continue; }
         u64 len = rec_len(x);
         Rec h = x;

@@ -87,22 +87,30 @@ def _exchange(send: torch.Tensor, send_units: List[int], group=None) -> Tuple[to
     return recv, recv_units
 
 
-def shuffle_reduce(engine, nreduce: int, group=None) -> int:
-    """Export the local aggregate by owner, all-to-all it, reduce the partitions this rank owns.
-    Returns the number of keys this rank owns.  `engine` holds the local map output."""
+def shuffle(engine, nreduce: int, group=None) -> None:
+    """The ihash shuffle: export the local aggregate by owner, all-to-all it, and import what
+    this rank owns.  Afterwards `engine` holds exactly the (aggregated) keys of the partitions
+    this rank owns (mapreduce.go:214-223 partitioning, :242-263 gathering)."""
     world = dist.get_world_size(group)
     send, units = engine.export_tensor(nreduce, world)
     recv, rcv_units = _exchange(send, units, group)
     engine.reset()
     engine.import_tensor(recv, sum(rcv_units))
+
+
+def shuffle_reduce(engine, nreduce: int, group=None) -> int:
+    """shuffle(), then DoReduce for the owned partitions (sorted and formatted on this rank).
+    Returns the number of keys this rank owns."""
+    shuffle(engine, nreduce, group)
     nkeys, _ = engine.reduce()
     return nkeys
 
 
-def gather_merge(engine, root_engine, root: int = 0, group=None) -> Optional[bytes]:
+def gather_merge(engine, root_engine, root: int = 0, group=None, fetch: bool = True) -> Optional[bytes]:
     """Merge (mapreduce.go:284-321) across ranks: every owner sends its keys to `root`, whose
     engine re-sorts the union (the owners' key sets are disjoint).  Returns the merged file
-    bytes on root, None elsewhere."""
+    bytes on root (fetch=False: leaves them in root_engine's device buffer and returns b""),
+    None elsewhere."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     send, units = engine.export_tensor(1, 1)
@@ -115,15 +123,19 @@ def gather_merge(engine, root_engine, root: int = 0, group=None) -> Optional[byt
     root_engine.reset()
     root_engine.import_tensor(recv, sum(rcv_units))
     root_engine.reduce()
-    return root_engine.result()
+    return root_engine.result() if fetch else b""
 
 
 class TorchEngine:
-    """wcg.Engine + torch buffers for the collectives (device memory stays in HBM)."""
+    """wcg.Engine + torch buffers for the collectives (device memory stays in HBM).
 
-    def __init__(self, engine, stream_ptr: int = 0):
+    host_staging=True hands the collectives host tensors instead (for the gloo backend, e.g.
+    several ranks sharing one GPU in a test; RCCL needs one GPU per rank)."""
+
+    def __init__(self, engine, stream_ptr: int = 0, host_staging: bool = False):
         self.e = engine
         self.stream = stream_ptr
+        self.host_staging = host_staging
 
     def reset(self):
         self.e.reset()
@@ -140,8 +152,11 @@ class TorchEngine:
         t = torch.empty(max(total, 1) * RECORD_BYTES, dtype=torch.uint8, device="cuda")
         device_copy(t.data_ptr(), ptr, total * RECORD_BYTES, self.stream)
         torch.cuda.current_stream().synchronize()
-        return t, counts
+        return (t.cpu() if self.host_staging else t), counts
 
     def import_tensor(self, t: torch.Tensor, nunits: int):
+        if not t.is_cuda:
+            t = t.to("cuda")
         torch.cuda.current_stream().synchronize()
         self.e.import_records(t.data_ptr(), nunits)
+        torch.cuda.current_stream().synchronize()     # t may be freed on return
