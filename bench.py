@@ -3,8 +3,10 @@
 
 A step = one word-count job over device-resident synthetic input (BASELINE.json config 2 per
 GPU: 1 GiB ASCII Zipf, V=1e5, s=1.0, seed 42; rank r gets the r-th GiB of the corpus): reset tables -> map kernel (tokenize +
-aggregate) -> [N > 1: export by owner, RCCL all-to-all-v, import + reduce owned partitions,
-gather to rank 0] -> sort + format the merged "key: count\\n" output in HBM.
+aggregate) -> [N > 1: export by owner, RCCL all-to-all-v, import the owned partitions, gather
+to rank 0] -> sort + format the merged "key: count\\n" output in HBM.  After the timed steps the
+merged file is checked byte for byte against the C oracle (N > 1: against the sum of every
+rank's oracle counts); a mismatch exits 3 without printing a rate.
 
   python bench.py --gpus N --steps K --warmup W
 N > 1 is launched by torch.distributed.run (one rank per GPU, backend nccl = RCCL).
@@ -34,7 +36,7 @@ def parse():
     ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30)
     ap.add_argument("--nreduce", type=int, default=64)
     ap.add_argument("--workload", default="c2_ascii_zipf_1gib")
-    ap.add_argument("--cpu-sample-mib", type=int, default=128)
+    ap.add_argument("--cpu-sample-mib", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),

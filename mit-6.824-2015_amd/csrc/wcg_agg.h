@@ -16,6 +16,7 @@ constexpr int AGG_NT = 1024;
 constexpr u32 AGG_BATCH = AGG_NT * 4;     // units per batch (4 per thread)
 constexpr int AGG_W = 2;               // ways per bucket (16-byte k0 rows: wcg_lds_table.h)
 constexpr int AGG_NB = 3380;           // 3380 x 2 slots x 24 B (u64 counts) = 162240 B (+ 1.5 KiB)
+constexpr u32 AGG_SLACK_UNITS = AGG_BATCH + 8;   // pool tail slack for k_agg's unmasked loads
 constexpr u32 AGG_MAX_SRC = 256;       // source regions per workgroup (+1 KiB LDS = 160 KiB)
 
 struct AggArgs {
@@ -60,10 +61,10 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
         const bool live = w < w1;
         const u32 i = b * AGG_BATCH + 4 * tid, lim = live ? rlen(w) : 0;
         const v4u* q = reinterpret_cast<const v4u*>(a.pool + ((u64)(live ? w : w0) * a.P + p) * a.region_cap + i);
-        const v4u z = {0, 0, 0, 0};
-        x0 = i < lim ? q[0] : z;
-        x1 = i + 2 < lim ? q[1] : z;
-        x2 = i + 4 < lim ? q[2] : z;
+        (void)lim;                    // units past the region's length are masked in process()
+        x0 = q[0];                    // unconditional (the pool has AGG_SLACK_UNITS of slack),
+        x1 = q[1];                    // so no branch splits the loads from the waits that let
+        x2 = q[2];                    // the next batch stay in flight
     };
     auto unit = [](const v4u& x, int h) -> u64 { return h ? ((u64)x.w << 32 | x.z) : ((u64)x.y << 32 | x.x); };
     auto process = [&](u32 w, u32 b, const v4u& x0, const v4u& x1, const v4u& x2) {

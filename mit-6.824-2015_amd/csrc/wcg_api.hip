@@ -309,7 +309,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // offsets fit 32 bits and its 24-bit multiplies (P * region_cap * 8 <= 2^31)
     a.region_cap = std::min<u64>(std::max<u64>(2048, per_wg_bytes / (8ull * P)), (1ull << 31) / (8ull * P)) & ~1ull;
     a.pmask = P - 1;
-    u64 need = grid * P * a.region_cap * sizeof(u64);
+    u64 need = (grid * P * a.region_cap + AGG_SLACK_UNITS) * sizeof(u64);
     if (need > c->pool_bytes) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (c->pool) HIPCHK(c, hipFree(c->pool));

@@ -1,7 +1,7 @@
 """Test-side access to the oracle (oracle/liboracle.so and oracle/wc_ref.py).
 
-Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module; the
-product never does.
+Only tests/, __graft_entry__.smoke() and bench.py (its cpu_baseline leg, and the result check
+after the timed region) use this module, always as the checker; the product never does.
 """
 from __future__ import annotations
 
