@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearsal of the N > 1 path with host-staged records, ranks may share a GPU")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per map launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -87,10 +89,16 @@ def main():
         if world == 1 and args.gpus > 1:
             print("bench.py: N>1 must be launched with torch.distributed.run", file=sys.stderr)
             sys.exit(2)
+    gloo = args.dist_backend == "gloo"
+    if gloo:                                  # rehearsal: ranks may share the box's GPU(s)
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     cfg = dict(CONFIGS[args.workload])
     n = args.bytes_per_gpu
@@ -105,25 +113,26 @@ def main():
     eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=max(4 * cfg["vocab"], 1 << 18))
     eng.set_stream(stream)
     eng.enable_timing(True)
-    teng = wd.TorchEngine(eng, stream)
+    teng = wd.TorchEngine(eng, stream, host_staging=gloo)
     root_eng = None
     if world > 1 and rank == 0:
         root_eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=max(4 * cfg["vocab"], 1 << 18))
         root_eng.set_stream(stream)
 
-    final = {}
-
     def step():
+        """one job; returns the device ms per phase of this rank's map (and, N = 1, reduce)"""
         eng.reset()
         eng.map_device(dev.data_ptr(), n)
         if world == 1:
             eng.reduce()
-            final["out"] = eng
-        else:
-            # owners need no sort of their own here: root re-sorts the union of the owners'
-            # disjoint key sets, and the merged file stays in root's HBM (fetched after timing)
-            wd.shuffle(teng, args.nreduce)
-            wd.gather_merge(teng, wd.TorchEngine(root_eng, stream) if root_eng else None, fetch=False)
+            return eng.timings()[0]
+        ph = eng.timings()[0]                 # taken before the shuffle's reset clears them
+        # owners need no sort of their own here: root re-sorts the union of the owners'
+        # disjoint key sets, and the merged file stays in root's HBM (fetched after timing)
+        wd.shuffle(teng, args.nreduce)
+        wd.gather_merge(teng, wd.TorchEngine(root_eng, stream, host_staging=gloo) if root_eng else None,
+                        fetch=False)
+        return ph
 
     for _ in range(args.warmup):
         step()
@@ -133,8 +142,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        ph = eng.timings()[0]
+        ph = step()
         map_ms.append(ph["map"])
         phase_ms.append(ph)
     torch.cuda.synchronize()
@@ -142,7 +150,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if gloo else "cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     stats = eng.stats() if world == 1 else None
@@ -180,7 +188,7 @@ def main():
         total_bytes = n * world
         gbs = total_bytes / (dt / args.steps) / 1e9
         avg_map_ms = sum(map_ms) / len(map_ms)
-        achieved = n / (avg_map_ms * 1e-3) / 1e9
+        achieved = n / (avg_map_ms * 1e-3) / 1e9 if avg_map_ms > 0 else None
         traffic = None
         try:
             with open(args.traffic_json) as f:
@@ -204,9 +212,14 @@ def main():
             "data": "synthetic (csrc/gencorpus.c; kjv12.txt absent)",
             "config": {"workload": args.workload, "bytes_per_gpu": n, "vocab": cfg["vocab"],
                        "zipf_s": cfg["zipf_s"], "seed": cfg["seed"], "nreduce": args.nreduce,
-                       "hbm_roofline_frac_whole_step": round(gbs / (HBM_PEAK_GBS * world), 4)},
-            "roofline": {"bound": "hbm", "kernel": "wcg::k_map", "achieved": round(achieved, 2),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                       "hbm_roofline_frac_whole_step": round(gbs / (HBM_PEAK_GBS * world), 4),
+                       "parallelism": f"{world} ranks, 1 GiB line-aligned range each",
+                       "shuffle": None if world == 1 else
+                       ("gloo rehearsal, host-staged" if gloo else "RCCL all_to_all_single (counts, then records)")},
+            "roofline": {"bound": "hbm", "kernel": "wcg::k_map",
+                         "achieved": round(achieved, 2) if achieved else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic, "avg_launch_ms": round(avg_map_ms, 4),
                          "algorithmic_bytes_per_launch": n},
         }
