@@ -72,6 +72,37 @@ def load() -> ctypes.CDLL:
     return lib
 
 
+_hiprt = None
+
+
+def _hip() -> ctypes.CDLL:
+    """The HIP runtime (plain copies between host buffers and libwcg's device buffers)."""
+    global _hiprt
+    if _hiprt is None:
+        for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+            try:
+                h = ctypes.CDLL(name)
+                break
+            except OSError:
+                continue
+        else:
+            raise ImportError("libamdhip64.so not found")
+        h.hipMemcpy.restype = ctypes.c_int
+        h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        h.hipMalloc.restype = ctypes.c_int
+        h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        h.hipFree.restype = ctypes.c_int
+        h.hipFree.argtypes = [ctypes.c_void_p]
+        h.hipDeviceSynchronize.restype = ctypes.c_int
+        _hiprt = h
+    return _hiprt
+
+
+def _hip_check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise WcgError(WCG_EHIP, f"{what} failed: hipError {rc}")
+
+
 def ihash(key: bytes) -> int:
     """FNV-1a 32 (mapreduce.go:185-189) via the library's host helper."""
     return load().wcg_ihash(key, len(key))
@@ -165,6 +196,33 @@ class Engine:
 
     def import_records(self, dev_ptr: int, nunits: int) -> None:
         self._chk(self._lib.wcg_import(self._ctx, ctypes.c_void_p(dev_ptr), nunits))
+
+    # -- host copies of the record units (the file-based shuffle of the config-5 workers)
+    def export_host(self, nreduce: int, nranks: int) -> Tuple[bytes, List[int]]:
+        """export() copied to host memory: (record units, units per rank)."""
+        ptr, counts = self.export(nreduce, nranks)
+        n = sum(counts) * RECORD_BYTES
+        buf = ctypes.create_string_buffer(max(n, 1))
+        if n:
+            _hip_check(_hip().hipMemcpy(buf, ctypes.c_void_p(ptr), n, 2), "hipMemcpy D2H")
+        return buf.raw[:n], counts
+
+    def import_host(self, records: bytes) -> None:
+        """import_records() from host memory (staged through a temporary device buffer)."""
+        if len(records) % RECORD_BYTES:
+            raise WcgError(WCG_EINVAL, "import_host: not a whole number of record units")
+        n = len(records) // RECORD_BYTES
+        if n == 0:
+            return
+        hip = _hip()
+        dev = ctypes.c_void_p()
+        _hip_check(hip.hipMalloc(ctypes.byref(dev), len(records)), "hipMalloc")
+        try:
+            _hip_check(hip.hipMemcpy(dev, records, len(records), 1), "hipMemcpy H2D")
+            self.import_records(dev.value, n)
+            _hip_check(hip.hipDeviceSynchronize(), "hipDeviceSynchronize")
+        finally:
+            hip.hipFree(dev)
 
     # -- diagnostics
     PHASES = ("map", "agg", "compact", "sort", "format")

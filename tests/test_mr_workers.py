@@ -1,0 +1,155 @@
+"""Config 5: master + workers over UNIX-socket RPC (wcg/mr.py), modelled on the reference's
+test_test.go (TestBasic / TestOneFailure / TestManyFailures, test_test.go:136-191).
+
+The CPU tests run the workers with a stand-in engine that speaks libwcg's record-unit format
+(the oracle's counts behind it). The `gpu` test runs the same master and workers on the real
+HIP engine. Every test checks:
+  * the merged file against the oracle, byte for byte;
+  * every -res-<r> file against the reference's DoReduce output;
+  * that CleanupFiles finds exactly the reference's file names.
+"""
+import os
+import threading
+import time
+
+import pytest
+
+from tests.oracle_bridge import wc_ref
+from tests.test_distributed import decode, encode
+
+
+class StandInEngine:
+    """wcg.Engine's job interface over the oracle (CPU tests only)."""
+
+    def __init__(self):
+        self.counts = {}
+
+    def reset(self):
+        self.counts = {}
+
+    def map_host(self, data):
+        for k, v in wc_ref.word_count(data).items():
+            self.counts[k] = self.counts.get(k, 0) + v
+
+    def export_host(self, nreduce, nranks):
+        buckets = [[] for _ in range(nranks)]
+        for k, c in self.counts.items():
+            buckets[(wc_ref.ihash(k) % nreduce) % nranks].append(encode(k, c))
+        parts = [b"".join(b) for b in buckets]
+        return b"".join(parts), [len(p) // 32 for p in parts]
+
+    def import_host(self, recs):
+        for k, c in decode(recs):
+            self.counts[k] = self.counts.get(k, 0) + c
+
+    def reduce(self):
+        return len(self.counts), 0
+
+    def partition(self, nreduce, r):
+        return wc_ref.res_file(self.counts, nreduce, r)
+
+
+def _input(tmp_path, nbytes=300_000):
+    from wcg.corpus import Generator
+    data = Generator(1, 20_000, 1.0, 31).bytes(nbytes)
+    data += b"carriage\r\nreturn lines\r\n" + "ǅungla ĳssel".encode() + b" tail-without-newline"
+    path = tmp_path / "824-mrinput.txt"
+    path.write_bytes(data)
+    return str(path), data
+
+
+def _expected(data):
+    # the parity input for the file path: Split's line handling (CR dropped, final \n added)
+    lines = data.split(b"\n")
+    if lines and lines[-1] == b"":
+        lines.pop()
+    text = b"".join((l[:-1] if l.endswith(b"\r") else l) + b"\n" for l in lines)
+    return wc_ref.word_count(text)
+
+
+def _run(tmp_path, factory, nmap, nreduce, schedule, timeout=240):
+    """schedule(master_addr, start_worker) starts workers (possibly over time)."""
+    from wcg import mr
+    path, data = _input(tmp_path)
+    sock = tmp_path / "sock"
+    sock.mkdir()
+    master = str(sock / "mr-master")
+    job = mr.MapReduce(nmap, nreduce, path, master, str(tmp_path))
+    workers = []
+
+    def start(nrpc):
+        w = mr.Worker(master, str(sock / f"mr-worker{len(workers)}"), factory, str(tmp_path), nrpc).start()
+        workers.append(w)
+        return w
+
+    stop = threading.Event()
+    t = threading.Thread(target=schedule, args=(start, stop), daemon=True)
+    t.start()
+    merged = job.wait(timeout)
+    stop.set()
+    t.join(10)
+    counts = _expected(data)
+    assert merged == wc_ref.merged_output(counts)
+    for r in range(nreduce):
+        with open(os.path.join(str(tmp_path), mr.merge_name(job.file, r)), "rb") as f:
+            assert f.read() == wc_ref.res_file(counts, nreduce, r)
+    job.cleanup_files()                     # every reference file name exists (else raises)
+    left = [f for f in os.listdir(tmp_path) if f.startswith("mrtmp.")]
+    assert left == [], left
+    return job, workers
+
+
+def _basic(start, stop):
+    start(-1)
+    start(-1)
+
+
+def _one_failure(start, stop):
+    start(10)                               # dies after 10 RPCs (worker.go:80-89)
+    start(-1)
+
+
+def _many_failures(start, stop):
+    while not stop.is_set():                # test_test.go:167-191: new 10-RPC workers keep coming
+        start(10)
+        start(10)
+        time.sleep(0.3)
+
+
+@pytest.mark.parametrize("name,schedule", [("basic", _basic), ("one_failure", _one_failure),
+                                           ("many_failures", _many_failures)])
+def test_master_workers_cpu_standin(tmp_path, name, schedule):
+    job, workers = _run(tmp_path, StandInEngine, nmap=20, nreduce=10, schedule=schedule)
+    if name == "basic":                     # checkWorker: every worker did at least one job
+        assert len(job.stats) == 2 and all(n > 0 for n in job.stats), job.stats
+
+
+def test_split_matches_reference_rules(tmp_path):
+    from wcg import mr
+    p = tmp_path / "in.txt"
+    p.write_bytes(b"ab cd\r\nef\n\ngh ij kl\nlast")
+    n = mr.split(str(p), 3, str(tmp_path), "in.txt")
+    parts = [(tmp_path / mr.map_name("in.txt", k)).read_bytes() for k in range(n)]
+    assert b"".join(parts) == b"ab cd\nef\n\ngh ij kl\nlast\n"
+    # size 25, nchunk = 25 // 3 + 1 = 9: a new split starts once more than 9 * m bytes were written
+    assert parts == [b"ab cd\nef\n\n", b"gh ij kl\n", b"last\n"]
+
+
+@pytest.mark.gpu
+def test_master_workers_gpu(tmp_path, built):
+    import wcg
+    _run(tmp_path, lambda: wcg.Engine(0, 1 << 20, 1 << 18), nmap=8, nreduce=5, schedule=_one_failure)
+
+
+@pytest.mark.gpu
+def test_run_single_gpu(tmp_path, built):
+    """RunSingle (mapreduce.go:344-356) on the GPU: -res-<r> files and the merged file."""
+    import wcg
+    from wcg import mr
+    path, data = _input(tmp_path)
+    with wcg.Engine(0, 1 << 20, 1 << 18) as e:
+        merged = mr.run_single(5, 3, path, e, str(tmp_path))
+    counts = _expected(data)
+    assert merged == wc_ref.merged_output(counts)
+    for r in range(3):
+        assert (tmp_path / mr.merge_name(os.path.basename(path), r)).read_bytes() == wc_ref.res_file(counts, 3, r)
