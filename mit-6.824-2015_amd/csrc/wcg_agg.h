@@ -47,19 +47,24 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     for (u32 w = w0 + tid; w < w1; w += AGG_NT) rlen_s[w - w0] = a.region_len[(u64)w * a.P + p];
     __syncthreads();
     u64 my_global = 0;
-    // Batches: thread t of a batch takes units [4t, 4t + 4) of one region and also loads the
-    // two after them, so a medium-key head or a count flag finds its neighbours in registers
-    // (units past the region's length are masked to 0 = filler).  The next batch is loaded into
-    // the other register set while this one is aggregated.  (Compiler-managed loads: the
-    // hand-counted asm loads of k_map measured no faster here.)
+    // Every wave walks its own regions (w0 + wave, + 16, ...) in wave batches of 256 units:
+    // lane l takes units [4l, 4l + 4) and also loads the two after them, so a medium-key head or
+    // a count flag finds its neighbours in registers (units past the region's length are masked
+    // to 0 = filler).  The next wave batch is loaded into the other register set while this one
+    // is aggregated, and no barrier ties the waves together, so 16 waves x 2 batches are in
+    // flight per CU: a workgroup-wide batch walk kept only 2, and k_agg ran at the HBM latency
+    // of one batch per region even for nearly empty regions.
+    const int wave = tid >> 6, lane = tid & 63;
+    constexpr u32 WB = 256;                          // units per wave batch
+    constexpr u32 WSTRIDE = AGG_NT / 64;             // regions between a wave's regions
     auto rlen = [&](u32 w) -> u32 { return rlen_s[w - w0]; };
     auto next_batch = [&](u32& w, u32& b) {          // wave-uniform walk over non-empty batches
         b++;
-        while (w < w1 && (u64)b * AGG_BATCH >= rlen(w)) { w++; b = 0; }
+        while (w < w1 && (u64)b * WB >= rlen(w)) { w += WSTRIDE; b = 0; }
     };
     auto load = [&](u32 w, u32 b, v4u& x0, v4u& x1, v4u& x2) {
         const bool live = w < w1;
-        const u32 i = b * AGG_BATCH + 4 * tid, lim = live ? rlen(w) : 0;
+        const u32 i = b * WB + 4 * lane, lim = live ? rlen(w) : 0;
         const v4u* q = reinterpret_cast<const v4u*>(a.pool + ((u64)(live ? w : w0) * a.P + p) * a.region_cap + i);
         (void)lim;                    // units past the region's length are masked in process()
         x0 = q[0];                    // unconditional (the pool has AGG_SLACK_UNITS of slack),
@@ -69,7 +74,7 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     auto unit = [](const v4u& x, int h) -> u64 { return h ? ((u64)x.w << 32 | x.z) : ((u64)x.y << 32 | x.x); };
     auto process = [&](u32 w, u32 b, const v4u& x0, const v4u& x1, const v4u& x2) {
         u64 u[6] = {unit(x0, 0), unit(x0, 1), unit(x1, 0), unit(x1, 1), unit(x2, 0), unit(x2, 1)};
-        const u32 i0 = b * AGG_BATCH + 4 * tid, len = rlen(w);
+        const u32 i0 = b * WB + 4 * lane, len = rlen(w);
 #pragma unroll
         for (int k = 0; k < 6; k++) u[k] = i0 + k < len ? u[k] : 0;
         u64 k0[4], k1[4], c[4];
@@ -99,7 +104,7 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
             }
         }
     };
-    u32 wa = w0, ba = (u32)-1;
+    u32 wa = w0 + wave, ba = (u32)-1;
     next_batch(wa, ba);
     u32 wb = wa, bb = ba;
     next_batch(wb, bb);
