@@ -110,13 +110,15 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream().cuda_stream
-    eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=max(4 * cfg["vocab"], 1 << 18))
+    # table capacity: the vocabulary, but no more keys than one per 16 input bytes could hold
+    keys_cap = max(min(4 * cfg["vocab"], n // 16), 1 << 18)
+    eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=keys_cap)
     eng.set_stream(stream)
     eng.enable_timing(True)
     teng = wd.TorchEngine(eng, stream, host_staging=gloo)
     root_eng = None
     if world > 1 and rank == 0:
-        root_eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=max(4 * cfg["vocab"], 1 << 18))
+        root_eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=keys_cap)
         root_eng.set_stream(stream)
 
     def step():

@@ -300,14 +300,15 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     a.ltab = c->ltab; a.lmask = c->lslots - 1;
     a.arena = c->arena; a.arena_cap = c->arena_cap;
     a.st = c->st;
-    // miss log: one region per (workgroup, bucket) of 8-byte units; the whole pool is ~n
-    // bytes, enough for ~0.7 misses per token of ordinary text; a full region falls back to
-    // the global table
+    // miss log: one region per (workgroup, bucket) of 8-byte units; the whole pool is ~2n
+    // bytes: a unit for every 4 input bytes covers every token missing the LDS table even on
+    // high-cardinality UTF-8 text (C4: 0.1 tokens per byte, 79% misses, 2-unit keys), where a
+    // 1-per-8 pool overflowed into per-token global-table inserts; only written units cost time
     const u32 P = c->nbuckets;
     u64 per_wg_bytes = (u64)a.tiles_per_wg * MAP_STEP;
     // even (16-byte aligned regions); a workgroup's regions stay under 2 GiB so k_map's unit
     // offsets fit 32 bits and its 24-bit multiplies (P * region_cap * 8 <= 2^31)
-    a.region_cap = std::min<u64>(std::max<u64>(2048, per_wg_bytes / (8ull * P)), (1ull << 31) / (8ull * P)) & ~1ull;
+    a.region_cap = std::min<u64>(std::max<u64>(2048, per_wg_bytes / (4ull * P)), (1ull << 31) / (8ull * P)) & ~1ull;
     a.pmask = P - 1;
     u64 need = (grid * P * a.region_cap + AGG_SLACK_UNITS) * sizeof(u64);
     if (need > c->pool_bytes) {

@@ -46,7 +46,7 @@ constexpr int MAP_STEP = 16 * MAP_OWN;       // 992 input bytes per wave step
 constexpr int MAP_WIN = 1024;                // bytes loaded per step: [step base - 16, + 1024)
 constexpr int MAP_WREG = MAP_WIN + 8;        // staging (+8: keyread's third word at the end)
 constexpr int MAP_SST = 512;                 // max token starts per step (992 / 2 = 496)
-constexpr int MAP_NS = 8960;                 // LDS short-key slots (12 B each)
+constexpr int MAP_NS = 8896;                 // LDS short-key slots (12 B each)
 constexpr int MAP_NM = 1024;                 // LDS medium-key slots (20 B each)
 #ifndef WCG_MAP_SETS
 #define WCG_MAP_SETS 4
@@ -100,6 +100,51 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* in, u64 n, long pos) 
     return v;
 }
 
+// count one long key (> 15 bytes: len, FNV-1a 64 h over its bytes) in the long-key table;
+// src(i) returns key byte i
+template <typename Src>
+__device__ __forceinline__ void ltab_add(const MapArgs& a, u64 len, u64 h, Src src) {
+    if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); return; }
+    u64 tag = mix64(h ^ len) | 1ull;
+    u64 s = tag & a.lmask, probes = 0;
+    int spins = 0;
+    while (true) {
+        GEntry* e = &a.ltab[s];
+        u64 c0 = ld_agent(&e->k0);
+        if (c0 == 0) {
+            u64 exp = 0;
+            if (cas_agent(&e->k0, &exp, tag)) {
+                u64 off = atomicAdd(&a.st->arena_top, len);
+                if (off + len > a.arena_cap) { atomicAdd(&a.st->overflow, 1u); return; }
+                for (u64 i = 0; i < len; i++) a.arena[off + i] = src(i);
+                st_agent(&e->aux, len);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __hip_atomic_store(&e->k1, off + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                add_agent(&e->cnt, 1);
+                return;
+            }
+            c0 = exp;
+        }
+        if (c0 == tag) {
+            u64 r = ld_agent(&e->k1);
+            if (r == 0) {
+                if (++spins > SPIN_LIMIT) { atomicAdd(&a.st->spin_fail, 1u); return; }
+                continue;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            bool same = ld_agent(&e->aux) == len;
+            if (same) {                 // all bytes at once: independent loads, no early exit
+                u32 diff = 0;
+                for (u64 i = 0; i < len; i++) diff |= (u32)a.arena[r - 1 + i] ^ (u32)src(i);
+                same = diff == 0;
+            }
+            if (same) { add_agent(&e->cnt, 1); return; }
+        }
+        s = (s + 1) & a.lmask;
+        if (++probes > a.lmask) { atomicAdd(&a.st->overflow, 1u); return; }
+    }
+}
+
 // long token (> 15 bytes, or a run k_map could not measure in its window) starting at absolute
 // offset p: walk runes in global memory
 __device__ void long_token(const MapArgs& a, u64 p) {
@@ -129,42 +174,27 @@ __device__ void long_token(const MapArgs& a, u64 p) {
         ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
         return;
     }
-    if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); return; }
-    u64 tag = mix64(h ^ len) | 1ull;
-    u64 s = tag & a.lmask, probes = 0;
-    int spins = 0;
+    ltab_add(a, len, h, [&](u64 i) -> uint8_t { return in[p + i]; });
+}
+
+// long token (> 15 bytes) starting at window offset rp (absolute offset p): its length from
+// the wave's chunk letter masks and its bytes from the staged window, both in LDS - a per-rune
+// walk through global memory is a chain of dependent loads per byte.  A run that reaches the
+// look-ahead chunk may continue past the window: that one takes the global walk.
+__device__ void long_token_win(const MapArgs& a, u64 p, u32 rp, const uint8_t* win, const uint16_t* wm) {
+    u32 c = rp >> 4, b = rp & 15, len = 0;
     while (true) {
-        GEntry* e = &a.ltab[s];
-        u64 c0 = ld_agent(&e->k0);
-        if (c0 == 0) {
-            u64 exp = 0;
-            if (cas_agent(&e->k0, &exp, tag)) {
-                u64 off = atomicAdd(&a.st->arena_top, len);
-                if (off + len > a.arena_cap) { atomicAdd(&a.st->overflow, 1u); return; }
-                for (u64 i = 0; i < len; i++) a.arena[off + i] = in[p + i];
-                st_agent(&e->aux, len);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                __hip_atomic_store(&e->k1, off + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                add_agent(&e->cnt, 1);
-                return;
-            }
-            c0 = exp;
-        }
-        if (c0 == tag) {
-            u64 r = ld_agent(&e->k1);
-            if (r == 0) {
-                if (++spins > SPIN_LIMIT) { atomicAdd(&a.st->spin_fail, 1u); return; }
-                continue;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            u64 elen = ld_agent(&e->aux);
-            bool same = (elen == len);
-            for (u64 i = 0; same && i < len; i++) same = (a.arena[r - 1 + i] == in[p + i]);
-            if (same) { add_agent(&e->cnt, 1); return; }
-        }
-        s = (s + 1) & a.lmask;
-        if (++probes > a.lmask) { atomicAdd(&a.st->overflow, 1u); return; }
+        if (c >= 63) { long_token(a, p); return; }
+        const u32 mm = (u32)wm[c] >> b;             // the chunk's bits from b on (zeros above)
+        const u32 t = __builtin_ctz(~mm);
+        if (t < 16 - b) { len += t; break; }
+        len += 16 - b;
+        c++;
+        b = 0;
     }
+    u64 h = 0xCBF29CE484222325ull;
+    for (u32 i = 0; i < len; i++) { h ^= win[rp + i]; h *= 0x100000001B3ull; }
+    ltab_add(a, len, h, [&](u64 i) -> uint8_t { return win[rp + i]; });
 }
 
 // 16-bit letter mask of the region chunk at byte `pos` of the wave's staged bytes (UTF-8 path)
@@ -230,6 +260,7 @@ template <int ABL>
 __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     __shared__ __align__(16) uint8_t wbytes[MAP_WAVES][MAP_WREG];
     __shared__ __align__(16) uint16_t wstart[MAP_WAVES][MAP_SST];
+    __shared__ uint16_t wmask[MAP_WAVES][64];   // chunk letter masks of the wave's window
     __shared__ __align__(16) u64 sk0[MAP_NS];
     __shared__ __align__(16) u64 mk0[MAP_NM];
     __shared__ __align__(16) u64 mk1[MAP_NM];
@@ -329,6 +360,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             if (lane == 63) m |= 0xE000u;
         }
         if (ABL == 4) { asm volatile("" ::"v"(m)); return 0; }
+        wmask[wave][lane] = (uint16_t)m;
         // neighbours' masks by DPP lane shifts
         const u32 prevm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x138, 0xF, 0xF, false);   // wave_shr:1
         const u32 nextm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x130, 0xF, 0xF, false);   // wave_shl:1
@@ -384,7 +416,11 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         };
         for (u32 it = 0; it < iters; it++) {
             if (ABL == 1) { sink += cur.e; cur.e = sst[(it + 1) * 64 + lane]; continue; }
-            if (cur.lng) { my_long++; long_token(a, (u64)(wbase + (cur.e & ((1u << SST_LEN_SHIFT) - 1)))); }
+            if (cur.lng) {
+                my_long++;
+                const u32 rp = cur.e & ((1u << SST_LEN_SHIFT) - 1);
+                long_token_win(a, (u64)(wbase + rp), rp, bytes, wmask[wave]);
+            }
             const bool med = !cur.shrt;
             const u64 k0 = (u64)cur.k0h << 32 | cur.k0l, k1 = (u64)cur.k1h << 32 | cur.k1l;
             if (ABL == 2) { sink += cur.h; cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, keyread(e_nxt));
