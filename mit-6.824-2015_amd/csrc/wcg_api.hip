@@ -50,6 +50,9 @@ struct wcg_ctx {
     u64* pool = nullptr; u64 pool_bytes = 0;
     u32* region_len = nullptr; u64 region_len_cap = 0;
     u64* wg_stats = nullptr; u64 wg_stats_cap = 0;   // k_map per-workgroup stats [grid][4]
+    // long-token log (k_map -> k_long): one region of {offset | len << 40} records per workgroup
+    u64* llog = nullptr; u64 llog_cap = 0;
+    u32* llog_len = nullptr; u64 llog_len_cap = 0;
     u32 nbuckets = 64;
     // timing
     bool timing = false;
@@ -171,7 +174,7 @@ int sort_records(wcg_ctx* c) {
 int format(wcg_ctx* c, int fmt, u32 nreduce, u32 part, uint8_t** dbuf, u64* cap, u64* nbytes) {
     const u64 n = c->nrec;
     if (n == 0) { *nbytes = 0; return WCG_OK; }
-    const u64 bound = n * (15 + JSON_FIXED + 20) + c->h_st->arena_top + 64;
+    const u64 bound = n * (LONG_CELL + JSON_FIXED + 20) + c->h_st->arena_top + 64;   // keys <= 32 B + heap keys
     int rc = ensure(c, dbuf, cap, bound);
     if (rc) return rc;
     const unsigned nt = (unsigned)((n + FM_TILE - 1) / FM_TILE);
@@ -216,12 +219,12 @@ int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx** 
     c->stream = c->own_stream;
     c->gslots = next_pow2(2 * c->max_keys);
     c->lslots = std::max<u64>(next_pow2(c->gslots / 4), 4096);
-    c->arena_cap = std::max<u64>(64ull << 20, c->lslots * 48);
+    c->arena_cap = std::max<u64>(64ull << 20, c->lslots * 32);   // heap part (after the slot cells)
     c->rec_cap = c->gslots / 2 + c->lslots / 2 + 16;
     if (c->max_input) HIPCHK(c, hipMalloc(&c->d_in, c->max_input + 64));
     HIPCHK(c, hipMalloc(&c->gtab, c->gslots * sizeof(GEntry)));
     HIPCHK(c, hipMalloc(&c->ltab, c->lslots * sizeof(GEntry)));
-    HIPCHK(c, hipMalloc(&c->arena, c->arena_cap + 64));
+    HIPCHK(c, hipMalloc(&c->arena, c->lslots * LONG_CELL + c->arena_cap + 64));
     HIPCHK(c, hipMalloc(&c->st, sizeof(DevState)));
     HIPCHK(c, hipHostMalloc(&c->h_st, sizeof(DevState), hipHostMallocDefault));
     // records: compaction output is bounded by the number of occupied slots
@@ -244,7 +247,7 @@ int wcg_close(wcg_ctx* c) {
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     void* bufs[] = {c->d_in, c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens,
                     c->d_scalar, c->d_out, c->d_part, c->owner, c->d_per_rank, c->exp_buf,
-                    c->pool, c->region_len, c->wg_stats};
+                    c->pool, c->region_len, c->wg_stats, c->llog, c->llog_len};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
@@ -332,6 +335,26 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         HIPCHK(c, hipMalloc(&c->wg_stats, grid * 4 * sizeof(u64)));
         c->wg_stats_cap = grid;
     }
+    // long-token log: a token > 15 bytes takes >= 17 input bytes, so a 992-byte step logs at
+    // most 59 of them; 60 records per step bound a workgroup's region
+    a.llog_cap = (u32)std::min<u64>((u64)a.tiles_per_wg * 60 + 64, 0xFFFFFFFFull);
+    const u64 lneed = grid * (u64)a.llog_cap * sizeof(u64);
+    if (lneed > c->llog_cap) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->llog) HIPCHK(c, hipFree(c->llog));
+        c->llog = nullptr; c->llog_cap = 0;
+        HIPCHK(c, hipMalloc(&c->llog, lneed));
+        c->llog_cap = lneed;
+    }
+    if (grid > c->llog_len_cap) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->llog_len) HIPCHK(c, hipFree(c->llog_len));
+        c->llog_len = nullptr; c->llog_len_cap = 0;
+        HIPCHK(c, hipMalloc(&c->llog_len, grid * sizeof(u32)));
+        c->llog_len_cap = grid;
+    }
+    a.llog = c->llog;
+    a.llog_len = c->llog_len;
     a.pool = c->pool;
     a.region_len = c->region_len;
     a.wg_stats = c->wg_stats;
@@ -344,10 +367,17 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         case 3: k_map<3><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
         case 4: k_map<4><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
         case 5: k_map<5><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
+        case 6: k_map<6><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
+        case 7: k_map<7><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
         default: k_map<0><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
     }
     HIPCHK(c, hipGetLastError());
     if (c->timing) { e1 = take_event(c); HIPCHK(c, hipEventRecord(e1, c->stream)); }
+    // the logged long tokens: LONG_PARTS workgroups per map workgroup's region
+    if (ablate == 0 || ablate >= 6) {
+        k_long<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, c->stream>>>(a, (u32)grid);
+        HIPCHK(c, hipGetLastError());
+    }
     AggArgs g;
     g.pool = c->pool; g.region_len = c->region_len; g.region_cap = a.region_cap;
     g.P = P; g.nsrc = (u32)grid;

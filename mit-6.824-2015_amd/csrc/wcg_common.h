@@ -55,6 +55,21 @@ constexpr u64 LONG_FLAG = 1ull << 63;
 constexpr u64 LONG_OFF_MASK = (1ull << 40) - 1;
 constexpr u64 LONG_LEN_MAX = (1ull << 23) - 1;
 
+// ---- long-key arena: [lslots x LONG_CELL-byte cells | heap].  A long key of <= LONG_CELL bytes
+// lives in the cell of the ltab slot that claimed it (no allocation, so no contended atomic on
+// one counter); a longer key gets a 16-byte aligned heap reservation (DevState::arena_top counts
+// heap bytes only).  Every key's bytes are zero-padded to its 16-byte cells, so readers compare
+// with 16-byte loads.
+constexpr u64 LONG_CELL = 32;
+__device__ __forceinline__ u64 long_cells(u64 len) { return len <= LONG_CELL ? LONG_CELL : (len + 15) & ~15ull; }
+// arena offset for a key claimed in slot s, or ~0 when the heap is full
+__device__ __forceinline__ u64 long_home(u64 s, u64 len, u64 lslots, u64 heap_cap, u64* arena_top) {
+    if (len <= LONG_CELL) return s * LONG_CELL;
+    const u64 r = long_cells(len);
+    const u64 ho = atomicAdd(arena_top, r);
+    return ho + r > heap_cap ? ~0ull : lslots * LONG_CELL + ho;
+}
+
 // ---- device-side counters/status (one per context)
 struct DevState {
     u64 tokens;          // tokens seen by map kernels
@@ -130,6 +145,58 @@ __device__ __forceinline__ u32 ascii_mask16(uint4 v) {
     return ascii_mask4(v.x) | (ascii_mask4(v.y) << 4) | (ascii_mask4(v.z) << 8) | (ascii_mask4(v.w) << 12);
 }
 __device__ __forceinline__ bool all_ascii(uint4 v) { return ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0; }
+
+// 4 bytes -> 4-bit mask of the bytes with the high bit set
+__device__ __forceinline__ u32 high_mask4(u32 x) {
+    return ((((x & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+// Letter test of a validly decoded non-ASCII code point.  The four largest all-letter blocks of
+// Unicode 13.0 (CJK Ext A 3400-4DBF, CJK 4E00-9FFC, Hangul AC00-D7A3, CJK Ext B 20000-2A6DD:
+// 62% of all letters; tests/test_oracle.py checks them against unicodedata 13.0) answer
+// from registers; every other code point reads the two-level table.
+__device__ __forceinline__ bool nonascii_letter(u32 cp) {
+    if ((cp - 0x4E00u) <= 0x9FFCu - 0x4E00u || (cp - 0xAC00u) <= 0xD7A3u - 0xAC00u ||
+        (cp - 0x3400u) <= 0x4DBFu - 0x3400u || (cp - 0x20000u) <= 0x2A6DDu - 0x20000u)
+        return true;
+    return lt_is_letter(cp);
+}
+
+// 16-bit letter mask of a chunk containing non-ASCII bytes, decoded from registers (fact F1):
+// `c` = the chunk, `pw` = the last 4 bytes before it, `nx` = the first 4 bytes after it (zeros
+// outside the input or the window).  Every non-continuation byte in [-3, 16) starts a rune in
+// Go's decoding; a valid letter rune marks all its bytes; every other byte is a non-letter
+// (utf8.RuneError, width 1).  Fully unrolled: each byte is a constant bit-field of six dwords.
+__device__ __forceinline__ u32 utf8_mask_regs(uint4 c, u32 pw, u32 nx) {
+    const u32 d[6] = {pw, c.x, c.y, c.z, c.w, nx};
+    // ASCII letters of the chunk (high-bit bytes masked off, then dropped)
+    u32 m = (ascii_mask4(c.x & 0x7F7F7F7Fu) & ~high_mask4(c.x)) |
+            ((ascii_mask4(c.y & 0x7F7F7F7Fu) & ~high_mask4(c.y)) << 4) |
+            ((ascii_mask4(c.z & 0x7F7F7F7Fu) & ~high_mask4(c.z)) << 8) |
+            ((ascii_mask4(c.w & 0x7F7F7F7Fu) & ~high_mask4(c.w)) << 12);
+#define WCG_B(j) ((d[((j) + 4) >> 2] >> (8 * (((j) + 4) & 3))) & 0xFFu)
+#pragma unroll
+    for (int i = -3; i < 16; i++) {
+        const u32 b0 = WCG_B(i);
+        if (b0 - 0xC2u <= 0xF4u - 0xC2u) {                 // a multi-byte lead (C2-F4)
+            const u32 b1 = WCG_B(i + 1), b2 = WCG_B(i + 2), b3 = WCG_B(i + 3);
+            const u32 w = b0 < 0xE0u ? 2u : (b0 < 0xF0u ? 3u : 4u);
+            const u32 lo = b0 == 0xE0u ? 0xA0u : (b0 == 0xF0u ? 0x90u : 0x80u);
+            const u32 hi = b0 == 0xEDu ? 0x9Fu : (b0 == 0xF4u ? 0x8Fu : 0xBFu);
+            const bool ok = b1 >= lo && b1 <= hi && (w < 3 || (b2 & 0xC0u) == 0x80u) &&
+                            (w < 4 || (b3 & 0xC0u) == 0x80u);
+            const u32 cp = w == 2 ? ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu)
+                         : w == 3 ? ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu)
+                                  : ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
+            if (ok && nonascii_letter(cp)) {
+                const u32 span = (1u << w) - 1u;
+                m |= i >= 0 ? span << i : span >> (-i);
+            }
+        }
+    }
+#undef WCG_B
+    return m & 0xFFFFu;
+}
 
 // ------------------------------------------------------------------ hashing
 __device__ __host__ __forceinline__ u64 mix64(u64 x) {

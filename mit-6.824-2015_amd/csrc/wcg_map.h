@@ -68,7 +68,10 @@ struct MapArgs {
     u32* region_len;               // units written per region
     u32 pmask;                     // P - 1 (P = number of miss buckets, power of two)
     u64* wg_stats;                 // [grid][4] per-workgroup {tokens, lds hits, global ops, long}
+    u64* llog;     u32 llog_cap;    // long-token log: region wg = llog[wg * llog_cap ...]
+    u32* llog_len;                 // records written per region
 };
+constexpr u64 LLOG_OFF_MASK = (1ull << 40) - 1;   // record = input offset | len << 40 (len 0: walk)
 
 // append one miss-log entry (wcg_lds_table.h) for this workgroup; false when the region is
 // full (the units of a region's last, cut-off entry are zeroed so k_agg skips them)
@@ -101,9 +104,11 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* in, u64 n, long pos) 
 }
 
 // count one long key (> 15 bytes: len, FNV-1a 64 h over its bytes) in the long-key table;
-// src(i) returns key byte i
-template <typename Src>
-__device__ __forceinline__ void ltab_add(const MapArgs& a, u64 len, u64 h, Src src) {
+// w(j) returns key word j (little-endian bytes 4j..4j+3, zeros past len).  Key bytes are
+// written and compared 16 bytes at a time against the zero-padded arena cells (wcg_common.h):
+// a byte loop over global memory is a chain of dependent loads per byte.
+template <typename W>
+__device__ __forceinline__ void ltab_add(const MapArgs& a, u64 len, u64 h, W w) {
     if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); return; }
     u64 tag = mix64(h ^ len) | 1ull;
     u64 s = tag & a.lmask, probes = 0;
@@ -114,9 +119,12 @@ __device__ __forceinline__ void ltab_add(const MapArgs& a, u64 len, u64 h, Src s
         if (c0 == 0) {
             u64 exp = 0;
             if (cas_agent(&e->k0, &exp, tag)) {
-                u64 off = atomicAdd(&a.st->arena_top, len);
-                if (off + len > a.arena_cap) { atomicAdd(&a.st->overflow, 1u); return; }
-                for (u64 i = 0; i < len; i++) a.arena[off + i] = src(i);
+                const u64 off = long_home(s, len, a.lmask + 1, a.arena_cap, &a.st->arena_top);
+                if (off == ~0ull) { atomicAdd(&a.st->overflow, 1u); return; }
+                const u64 cells = long_cells(len);
+                for (u64 j = 0; j < cells; j += 16)
+                    *reinterpret_cast<uint4*>(a.arena + off + j) =
+                        make_uint4(w(j / 4), w(j / 4 + 1), w(j / 4 + 2), w(j / 4 + 3));
                 st_agent(&e->aux, len);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 __hip_atomic_store(&e->k1, off + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -133,9 +141,12 @@ __device__ __forceinline__ void ltab_add(const MapArgs& a, u64 len, u64 h, Src s
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             bool same = ld_agent(&e->aux) == len;
-            if (same) {                 // all bytes at once: independent loads, no early exit
+            if (same) {                 // 16-byte cells, zero-padded on both sides
                 u32 diff = 0;
-                for (u64 i = 0; i < len; i++) diff |= (u32)a.arena[r - 1 + i] ^ (u32)src(i);
+                for (u64 j = 0; j < len; j += 16) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(a.arena + r - 1 + j);
+                    diff |= (v.x ^ w(j / 4)) | (v.y ^ w(j / 4 + 1)) | (v.z ^ w(j / 4 + 2)) | (v.w ^ w(j / 4 + 3));
+                }
                 same = diff == 0;
             }
             if (same) { add_agent(&e->cnt, 1); return; }
@@ -174,17 +185,29 @@ __device__ void long_token(const MapArgs& a, u64 p) {
         ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
         return;
     }
-    ltab_add(a, len, h, [&](u64 i) -> uint8_t { return in[p + i]; });
+    ltab_add(a, len, h, [&](u64 j) -> u32 {
+        u32 v = 0;
+        for (u64 k = 0; k < 4; k++)
+            if (4 * j + k < len) v |= (u32)in[p + 4 * j + k] << (8 * k);
+        return v;
+    });
 }
 
 // long token (> 15 bytes) starting at window offset rp (absolute offset p): its length from
 // the wave's chunk letter masks and its bytes from the staged window, both in LDS - a per-rune
 // walk through global memory is a chain of dependent loads per byte.  A run that reaches the
 // look-ahead chunk may continue past the window: that one takes the global walk.
-__device__ void long_token_win(const MapArgs& a, u64 p, u32 rp, const uint8_t* win, const uint16_t* wm) {
+// long token (> 15 bytes) starting at window offset rp (absolute offset p): its length from the
+// wave's chunk letter masks (LDS), then one record in the workgroup's long-token log; k_long
+// counts it.  A run that reaches the look-ahead chunk may continue past the window: its record
+// has length 0 and k_long walks its runes.  The global-table work stays out of k_map's token
+// loop: a dependent global load there waits for every older load of the wave, which drains the
+// window prefetch (measured: 40 ms of 47 per GiB of C4 text with the insert done here).
+template <int ABL = 0>
+__device__ __forceinline__ void long_token_log(const MapArgs& a, u64 p, u32 rp, const uint16_t* wm, u32* lcur) {
     u32 c = rp >> 4, b = rp & 15, len = 0;
     while (true) {
-        if (c >= 63) { long_token(a, p); return; }
+        if (c >= 63) { len = 0; break; }
         const u32 mm = (u32)wm[c] >> b;             // the chunk's bits from b on (zeros above)
         const u32 t = __builtin_ctz(~mm);
         if (t < 16 - b) { len += t; break; }
@@ -192,19 +215,50 @@ __device__ void long_token_win(const MapArgs& a, u64 p, u32 rp, const uint8_t* w
         c++;
         b = 0;
     }
-    u64 h = 0xCBF29CE484222325ull;
-    for (u32 i = 0; i < len; i++) { h ^= win[rp + i]; h *= 0x100000001B3ull; }
-    ltab_add(a, len, h, [&](u64 i) -> uint8_t { return win[rp + i]; });
+    if (ABL == 7) { asm volatile("" ::"v"(len)); return; }
+    const u32 pos = atomicAdd(lcur, 1u);
+    if (pos < a.llog_cap) a.llog[(u64)blockIdx.x * a.llog_cap + pos] = p | (u64)len << 40;
+    else atomicAdd(&a.st->overflow, 1u);           // cannot happen: 60 records per step bound it
 }
 
-// 16-bit letter mask of the region chunk at byte `pos` of the wave's staged bytes (UTF-8 path)
-template <typename At>
-__device__ __forceinline__ u32 utf8_mask(At at, int pos, int from) {
-    u32 m = 0;
-#pragma unroll 1
-    for (int i = from; i < 16; i++)
-        if (letter_byte(at, (long)(pos + i))) m |= 1u << i;
-    return m;
+// k_long: count the logged long tokens in the long-key table.  Workgroup b serves map region
+// b % nreg, with its LONG_PARTS workgroups striding over the region's records.  Key words come
+// from the resident input (two aligned loads + alignbyte, bytes past the key masked to zero).
+constexpr int LONG_NT = 256;
+constexpr int LONG_PARTS = 8;
+__global__ __launch_bounds__(LONG_NT) void k_long(MapArgs a, u32 nreg) {
+    const u32 reg = blockIdx.x % nreg, part = blockIdx.x / nreg;
+    const u32 nrec = a.llog_len[reg];
+    const u64* recs = a.llog + (u64)reg * a.llog_cap;
+    for (u32 i = part * LONG_NT + threadIdx.x; i < nrec; i += LONG_PARTS * LONG_NT) {
+        const u64 r = recs[i];
+        const u64 p = r & LLOG_OFF_MASK;
+        const u32 len = (u32)(r >> 40);
+        if (len == 0) { long_token(a, p); continue; }
+        const uint8_t* in = a.in;
+        const u64 n = a.n;
+        auto word = [&](u64 j) -> u32 {
+            if (4 * (u32)j >= len) return 0u;
+            const u64 base = p + 4 * j, q = base & ~3ull;
+            const u32 rem = len - 4 * (u32)j;
+            u32 v;
+            if (q + 8 <= n) {
+                const u32* wq = reinterpret_cast<const u32*>(in + q);
+                v = __builtin_amdgcn_alignbyte(wq[1], wq[0], (u32)(base & 3));
+            } else {
+                v = 0;
+                for (u32 k = 0; k < 4 && k < rem; k++) v |= (u32)in[base + k] << (8 * k);
+            }
+            return rem >= 4 ? v : v & ((1u << (8 * rem)) - 1);
+        };
+        u64 h = 0xCBF29CE484222325ull;
+        for (u32 j = 0; 4 * j < len; j++) {
+            const u32 v = word(j);
+            const u32 nb = len - 4 * j < 4 ? len - 4 * j : 4;
+            for (u32 k = 0; k < nb; k++) { h ^= (v >> (8 * k)) & 0xFFu; h *= 0x100000001B3ull; }
+        }
+        ltab_add(a, len, h, word);
+    }
 }
 
 // wave-local ordering of LDS accesses between lanes (the LDS executes one wave's
@@ -255,7 +309,8 @@ constexpr u32 OOB = 0xFFFFFFF0u;
 
 // ABL (measurement builds only, selected by WCG_MAP_ABLATE; results are wrong when ABL != 0):
 //   5 = input loads only, 4 = + LDS staging and letter masks, 1 = + token starts and compaction,
-//   2 = + key extraction and hash, 3 = + LDS lookup with misses dropped
+//   2 = + key extraction and hash, 3 = + LDS lookup with misses dropped; 6 = full but long
+//   tokens only counted, 7 = full but long tokens only measured and hashed
 template <int ABL>
 __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     __shared__ __align__(16) uint8_t wbytes[MAP_WAVES][MAP_WREG];
@@ -268,12 +323,14 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     __shared__ u32 scnt[MAP_NS];
     __shared__ u32 mcnt[MAP_NM];
     __shared__ u32 cursor[MAX_MISS_BUCKETS];
+    __shared__ u32 lcur;                        // long-token log cursor
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);     // wave-uniform (scalar)
     MapTable<MAP_NS, MAP_NM> tab{sk0, scnt, mk0, mk1, mcnt, &zero_w};
     tab.init(tid, MAP_NT);
     for (int i = tid; i < MAX_MISS_BUCKETS; i += MAP_NT) cursor[i] = 0;
+    if (tid == 0) lcur = 0;
     __syncthreads();
 
     uint8_t* const bytes = wbytes[wave];
@@ -350,13 +407,14 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         //      the step's first byte; lane 63: only as the successor of chunk 62, and on the
         //      UTF-8 path its last 3 bits, whose runes may end past the window, are forced to
         //      letters, so a run reaching them is measured exactly by the long-token path)
+        // the neighbour chunks' edge dwords by DPP (all lanes active; lane 0 / 63 get zeros)
+        const u32 pw = (u32)__builtin_amdgcn_update_dpp(0, (int)mine.w, 0x138, 0xF, 0xF, false);   // wave_shr:1
+        const u32 nx = (u32)__builtin_amdgcn_update_dpp(0, (int)mine.x, 0x130, 0xF, 0xF, false);   // wave_shl:1
         u32 m;
         if (all_ascii(mine)) {
             m = ascii_mask16(mine);
         } else {
-            wave_lds_sync();
-            auto at = [&](long i) -> u32 { return (i >= 0 && i < MAP_WIN) ? (u32)bytes[i] : 0u; };
-            m = utf8_mask(at, 16 * lane, lane == 0 ? 12 : 0);
+            m = utf8_mask_regs(mine, pw, nx);
             if (lane == 63) m |= 0xE000u;
         }
         if (ABL == 4) { asm volatile("" ::"v"(m)); return 0; }
@@ -419,7 +477,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             if (cur.lng) {
                 my_long++;
                 const u32 rp = cur.e & ((1u << SST_LEN_SHIFT) - 1);
-                long_token_win(a, (u64)(wbase + rp), rp, bytes, wmask[wave]);
+                if (ABL != 6) long_token_log<ABL>(a, (u64)(wbase + rp), rp, wmask[wave], &lcur);
             }
             const bool med = !cur.shrt;
             const u64 k0 = (u64)cur.k0h << 32 | cur.k0l, k1 = (u64)cur.k1h << 32 | cur.k1l;
@@ -442,10 +500,10 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, nkw);
             e_nxt = e_nn;
         }
-        if (ABL == 0) store_pending();
+        if (ABL == 0 || ABL >= 6) store_pending();
         if (ABL) asm volatile("" ::"v"(sink));
         wave_lds_sync();
-        return (ABL == 0) ? iters + 1 : 0u;
+        return (ABL == 0 || ABL >= 6) ? iters + 1 : 0u;
     };
 
     // ---- main loop, unrolled over the register sets so that each set's load and waits name
@@ -507,6 +565,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     for (int i = tid; i < MAP_NS; i += MAP_NT) flush(sk0[i], 0, scnt[i]);
     for (int i = tid; i < MAP_NM; i += MAP_NT) flush(mk0[i], mk1[i], mcnt[i]);
     __syncthreads();
+    if (tid == 0) a.llog_len[blockIdx.x] = lcur < a.llog_cap ? lcur : a.llog_cap;
     for (u32 p = tid; p <= a.pmask; p += MAP_NT) {
         const u32 c = cursor[p];
         a.region_len[(u64)blockIdx.x * (a.pmask + 1) + p] = c < a.region_cap ? c : (u32)a.region_cap;

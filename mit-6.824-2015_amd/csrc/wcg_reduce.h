@@ -473,9 +473,10 @@ __global__ void k_import(const Rec* in, u64 n, GEntry* gtab, u64 gmask, GEntry* 
             if (c0 == 0) {
                 u64 exp = 0;
                 if (cas_agent(&e->k0, &exp, tag)) {
-                    u64 off = atomicAdd(&st->arena_top, len);
-                    if (off + len > arena_cap) { atomicAdd(&st->overflow, 1u); break; }
-                    for (u64 k = 0; k < len; k++) arena[off + k] = cont_byte(src, k);
+                    const u64 off = long_home(s, len, lmask + 1, arena_cap, &st->arena_top);
+                    if (off == ~0ull) { atomicAdd(&st->overflow, 1u); break; }
+                    const u64 cells = long_cells(len);
+                    for (u64 k = 0; k < cells; k++) arena[off + k] = k < len ? cont_byte(src, k) : 0;
                     st_agent(&e->aux, len);
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                     st_agent(&e->k1, off + 1);
