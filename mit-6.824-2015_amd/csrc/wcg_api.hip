@@ -375,7 +375,8 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     if (c->timing) { e1 = take_event(c); HIPCHK(c, hipEventRecord(e1, c->stream)); }
     // the logged long tokens: LONG_PARTS workgroups per map workgroup's region
     if (ablate == 0 || ablate >= 6) {
-        k_long<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, c->stream>>>(a, (u32)grid);
+        static const int lab = getenv("WCG_LONG_ABLATE") ? atoi(getenv("WCG_LONG_ABLATE")) : 0;
+        k_long<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, c->stream>>>(a, (u32)grid, lab);
         HIPCHK(c, hipGetLastError());
     }
     AggArgs g;

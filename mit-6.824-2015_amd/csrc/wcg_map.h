@@ -107,9 +107,10 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* in, u64 n, long pos) 
 // w(j) returns key word j (little-endian bytes 4j..4j+3, zeros past len).  Key bytes are
 // written and compared 16 bytes at a time against the zero-padded arena cells (wcg_common.h):
 // a byte loop over global memory is a chain of dependent loads per byte.
+// Returns the slot that counted the key + 1 (0 when nothing was counted) and its arena offset.
 template <typename W>
-__device__ __forceinline__ void ltab_add(const MapArgs& a, u64 len, u64 h, W w) {
-    if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); return; }
+__device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 h, W w, int mode = 0, u64* arena_off = nullptr) {
+    if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); return 0; }
     u64 tag = mix64(h ^ len) | 1ull;
     u64 s = tag & a.lmask, probes = 0;
     int spins = 0;
@@ -120,7 +121,7 @@ __device__ __forceinline__ void ltab_add(const MapArgs& a, u64 len, u64 h, W w) 
             u64 exp = 0;
             if (cas_agent(&e->k0, &exp, tag)) {
                 const u64 off = long_home(s, len, a.lmask + 1, a.arena_cap, &a.st->arena_top);
-                if (off == ~0ull) { atomicAdd(&a.st->overflow, 1u); return; }
+                if (off == ~0ull) { atomicAdd(&a.st->overflow, 1u); return 0; }
                 const u64 cells = long_cells(len);
                 for (u64 j = 0; j < cells; j += 16)
                     *reinterpret_cast<uint4*>(a.arena + off + j) =
@@ -129,14 +130,15 @@ __device__ __forceinline__ void ltab_add(const MapArgs& a, u64 len, u64 h, W w) 
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 __hip_atomic_store(&e->k1, off + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 add_agent(&e->cnt, 1);
-                return;
+                if (arena_off) *arena_off = off;
+                return s + 1;
             }
             c0 = exp;
         }
         if (c0 == tag) {
             u64 r = ld_agent(&e->k1);
             if (r == 0) {
-                if (++spins > SPIN_LIMIT) { atomicAdd(&a.st->spin_fail, 1u); return; }
+                if (++spins > SPIN_LIMIT) { atomicAdd(&a.st->spin_fail, 1u); return 0; }
                 continue;
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -149,10 +151,14 @@ __device__ __forceinline__ void ltab_add(const MapArgs& a, u64 len, u64 h, W w) 
                 }
                 same = diff == 0;
             }
-            if (same) { add_agent(&e->cnt, 1); return; }
+            if (same) {
+                if (mode != 2) add_agent(&e->cnt, 1);
+                if (arena_off) *arena_off = r - 1;
+                return s + 1;
+            }
         }
         s = (s + 1) & a.lmask;
-        if (++probes > a.lmask) { atomicAdd(&a.st->overflow, 1u); return; }
+        if (++probes > a.lmask) { atomicAdd(&a.st->overflow, 1u); return 0; }
     }
 }
 
@@ -222,43 +228,103 @@ __device__ __forceinline__ void long_token_log(const MapArgs& a, u64 p, u32 rp, 
 }
 
 // k_long: count the logged long tokens in the long-key table.  Workgroup b serves map region
-// b % nreg, with its LONG_PARTS workgroups striding over the region's records.  Key words come
-// from the resident input (two aligned loads + alignbyte, bytes past the key masked to zero).
+// b % nreg, with its LONG_PARTS workgroups striding over the region's records in rounds of
+// LONG_NT.  Key words come from the resident input (two aligned loads + alignbyte, bytes past
+// the key masked to zero).
+// Hot keys: one count atomic per occurrence serialises on the key's slot (C4: the top long key
+// occurs 1.2e5 times per GiB; the count atomics were 5 of k_long's 12 ms).  A workgroup caches
+// {tag, len, slot, arena offset} of the keys it has counted in LDS; an occurrence whose tag and
+// length match a cached key compares its bytes with the key's arena cell (exact, 16-byte loads)
+// and counts in LDS; the LDS counts are added to the table once at the end.  Cache entries are
+// filled in one round and read only in later rounds (after the round's barrier), so no lane
+// waits on another's LDS write.
 constexpr int LONG_NT = 256;
 constexpr int LONG_PARTS = 8;
-__global__ __launch_bounds__(LONG_NT) void k_long(MapArgs a, u32 nreg) {
+constexpr int LCACHE = 1024;                  // LDS cache entries (28 B each)
+// mode (measurement only, WCG_LONG_ABLATE; results are wrong when mode != 0): 1 = hash only,
+// 2 = no count atomic on a hit, 3 = no LDS cache
+__global__ __launch_bounds__(LONG_NT) void k_long(MapArgs a, u32 nreg, int mode) {
+    __shared__ u64 ctag[LCACHE];
+    __shared__ u64 coff[LCACHE];              // arena offset + 1 (0 = not filled)
+    __shared__ u32 cslot[LCACHE], clen[LCACHE], ccnt[LCACHE];
+    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; coff[e] = 0; ccnt[e] = 0; }
+    __syncthreads();
     const u32 reg = blockIdx.x % nreg, part = blockIdx.x / nreg;
     const u32 nrec = a.llog_len[reg];
     const u64* recs = a.llog + (u64)reg * a.llog_cap;
-    for (u32 i = part * LONG_NT + threadIdx.x; i < nrec; i += LONG_PARTS * LONG_NT) {
-        const u64 r = recs[i];
+    const u32 stride = LONG_PARTS * LONG_NT, first = part * LONG_NT;
+    const u32 rounds = nrec > first ? (nrec - first + stride - 1) / stride : 0;   // workgroup-uniform
+    const uint8_t* in = a.in;
+    const u64 n = a.n;
+    for (u32 k = 0; k < rounds; k++) {
+        const u32 i = first + k * stride + threadIdx.x;
+        const u64 r = i < nrec ? recs[i] : 0;
         const u64 p = r & LLOG_OFF_MASK;
         const u32 len = (u32)(r >> 40);
-        if (len == 0) { long_token(a, p); continue; }
-        const uint8_t* in = a.in;
-        const u64 n = a.n;
-        auto word = [&](u64 j) -> u32 {
-            if (4 * (u32)j >= len) return 0u;
-            const u64 base = p + 4 * j, q = base & ~3ull;
-            const u32 rem = len - 4 * (u32)j;
-            u32 v;
-            if (q + 8 <= n) {
-                const u32* wq = reinterpret_cast<const u32*>(in + q);
-                v = __builtin_amdgcn_alignbyte(wq[1], wq[0], (u32)(base & 3));
-            } else {
-                v = 0;
-                for (u32 k = 0; k < 4 && k < rem; k++) v |= (u32)in[base + k] << (8 * k);
+        if (i < nrec && len == 0) long_token(a, p);
+        if (len != 0) {
+            auto word = [&](u64 j) -> u32 {
+                if (4 * (u32)j >= len) return 0u;
+                const u64 base = p + 4 * j, q = base & ~3ull;
+                const u32 rem = len - 4 * (u32)j;
+                u32 v;
+                if (q + 8 <= n) {
+                    const u32* wq = reinterpret_cast<const u32*>(in + q);
+                    v = __builtin_amdgcn_alignbyte(wq[1], wq[0], (u32)(base & 3));
+                } else {
+                    v = 0;
+                    for (u32 b = 0; b < 4 && b < rem; b++) v |= (u32)in[base + b] << (8 * b);
+                }
+                return rem >= 4 ? v : v & ((1u << (8 * rem)) - 1);
+            };
+            u64 h = 0xCBF29CE484222325ull;
+            for (u32 j = 0; 4 * j < len; j++) {
+                const u32 v = word(j);
+                const u32 nb = len - 4 * j < 4 ? len - 4 * j : 4;
+                for (u32 b = 0; b < nb; b++) { h ^= (v >> (8 * b)) & 0xFFu; h *= 0x100000001B3ull; }
             }
-            return rem >= 4 ? v : v & ((1u << (8 * rem)) - 1);
-        };
-        u64 h = 0xCBF29CE484222325ull;
-        for (u32 j = 0; 4 * j < len; j++) {
-            const u32 v = word(j);
-            const u32 nb = len - 4 * j < 4 ? len - 4 * j : 4;
-            for (u32 k = 0; k < nb; k++) { h ^= (v >> (8 * k)) & 0xFFu; h *= 0x100000001B3ull; }
+            if (mode == 1) { if (h == 0) atomicAdd(&a.st->overflow, 1u); }
+            else {
+                const u64 tag = mix64(h ^ len) | 1ull;
+                const u32 c0 = (u32)(tag >> 24) & (LCACHE - 1);
+                bool done = false;
+                if (mode == 0) {
+                    for (u32 q = 0; q < 4; q++) {                 // cached keys (earlier rounds)
+                        const u32 cs = (c0 + q) & (LCACHE - 1);
+                        const u64 t = ctag[cs];
+                        if (t == 0) break;
+                        if (t != tag) continue;
+                        const u64 off = coff[cs];
+                        if (off == 0 || clen[cs] != len) continue;
+                        u32 diff = 0;
+                        for (u64 j = 0; j < len; j += 16) {
+                            const uint4 v = *reinterpret_cast<const uint4*>(a.arena + off - 1 + j);
+                            diff |= (v.x ^ word(j / 4)) | (v.y ^ word(j / 4 + 1)) | (v.z ^ word(j / 4 + 2)) | (v.w ^ word(j / 4 + 3));
+                        }
+                        if (diff == 0) { atomicAdd(&ccnt[cs], 1u); done = true; }
+                        break;
+                    }
+                }
+                if (!done) {
+                    u64 off = 0;
+                    const u64 s1 = ltab_add(a, len, h, word, mode, &off);
+                    if (mode == 0 && s1) {                         // cache it for later rounds
+                        for (u32 q = 0; q < 4; q++) {
+                            const u32 cs = (c0 + q) & (LCACHE - 1);
+                            const u64 t = atomicCAS((unsigned long long*)&ctag[cs], 0ull, (unsigned long long)tag);
+                            if (t == 0) { coff[cs] = off + 1; cslot[cs] = (u32)(s1 - 1); clen[cs] = len; break; }
+                            if (t == tag) break;
+                        }
+                    }
+                }
+            }
         }
-        ltab_add(a, len, h, word);
+        __syncthreads();
+        // the arena cells read from the cache were written by other CUs: drop stale L1 lines
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
+    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT)
+        if (ccnt[e]) add_agent(&a.ltab[cslot[e]].cnt, (u64)ccnt[e]);
 }
 
 // wave-local ordering of LDS accesses between lanes (the LDS executes one wave's
