@@ -124,6 +124,27 @@ def test_long_keys_and_prefix_ties(eng):
     assert gpu_wc(eng, d) == ob.merged(d)
 
 
+def test_long_keys_hot_cached_and_cell_sizes(eng):
+    """k_long: hot long keys counted through the workgroup LDS cache over many rounds, keys at
+    the arena cell boundaries (16, 32 bytes in a slot cell; 33+ on the heap) that differ only in
+    their last byte, UTF-8 long keys, and the same keys again in a second map call (cells and
+    slots kept, cache rebuilt per launch)."""
+    rng = random.Random(17)
+    base = {L: b"k" * (L - 1) for L in (16, 17, 31, 32, 33, 47, 48, 49, 200)}
+    vocab = [b + bytes([c]) for b in base.values() for c in b"abcXYZ"]
+    vocab += [("λέξη" * 3 + "中文字符" + "한국어" + s).encode() for s in ("a", "b", "ab", "")]
+    hot = vocab[:3]
+    words = []
+    for _ in range(400_000):
+        words.append(rng.choice(hot) if rng.random() < 0.6 else rng.choice(vocab))
+    d = b" ".join(words) + b"\n"
+    want = ob.merged(d)
+    assert gpu_wc(eng, d) == want
+    assert gpu_wc(eng, d, splits=3) == want
+    st = eng.stats()
+    assert st["long_tokens"] == 400_000 and st["overflow"] == 0 and st["spin_fail"] == 0
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_corpus_multi_split(eng, mode):
     from wcg.corpus import Generator
