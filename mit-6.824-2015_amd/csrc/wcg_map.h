@@ -116,7 +116,12 @@ __device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 h, W w, i
     int spins = 0;
     while (true) {
         GEntry* e = &a.ltab[s];
+        // the entry's three words in one round trip (independent loads); aux (the length) is
+        // written once, before the release that publishes k1: a 0 read here is re-read after
+        // the acquire, any other value is final
         u64 c0 = ld_agent(&e->k0);
+        u64 r = ld_agent(&e->k1);
+        u64 elen = ld_agent(&e->aux);
         if (c0 == 0) {
             u64 exp = 0;
             if (cas_agent(&e->k0, &exp, tag)) {
@@ -134,15 +139,16 @@ __device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 h, W w, i
                 return s + 1;
             }
             c0 = exp;
+            r = ld_agent(&e->k1);
         }
         if (c0 == tag) {
-            u64 r = ld_agent(&e->k1);
             if (r == 0) {
                 if (++spins > SPIN_LIMIT) { atomicAdd(&a.st->spin_fail, 1u); return 0; }
                 continue;
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            bool same = ld_agent(&e->aux) == len;
+            if (elen == 0) elen = ld_agent(&e->aux);
+            bool same = elen == len;
             if (same) {                 // 16-byte cells, zero-padded on both sides
                 u32 diff = 0;
                 for (u64 j = 0; j < len; j += 16) {
