@@ -110,8 +110,11 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream().cuda_stream
-    # table capacity: the vocabulary, but no more keys than one per 16 input bytes could hold
-    keys_cap = max(min(4 * cfg["vocab"], n // 16), 1 << 18)
+    # table capacity: the vocabulary, but no more keys than one per 32 input bytes (C4's densest
+    # slice has one distinct key per 45 bytes).  Oversized tables cost time: k_compact scans every
+    # slot, and the table probes of k_agg/k_long spread over more pages (TLB) and miss the
+    # 256 MB MALL.  A table too small for the input fails loudly (WCG_EFULL), never silently.
+    keys_cap = max(min(4 * cfg["vocab"], n // 32), 1 << 18)
     eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=keys_cap)
     eng.set_stream(stream)
     eng.enable_timing(True)
