@@ -109,13 +109,16 @@ WCG_API int wcg_import(wcg_ctx *ctx, const void *dev_records, uint64_t nrecords)
 
 /* Per-phase device time of the last pipeline run, in milliseconds, measured with HIP events
  * on the context's stream: ms[0] map kernel (tokenize + LDS aggregation, summed over the
- * wcg_map* calls since wcg_reset), ms[1] miss-log aggregation kernel, ms[2] compaction,
+ * wcg_map* calls since wcg_reset), ms[1] long-token counting + miss-log aggregation kernels
+ * (k_long, k_agg), ms[2] compaction,
  * ms[3] sort, ms[4] format.  n = number of doubles the caller provides (<= 5). */
 WCG_API int wcg_timings(wcg_ctx *ctx, double *ms, int n, uint64_t *map_launches);
 /* Enable/disable the event timing above (off by default: it adds event records). */
 WCG_API int wcg_enable_timing(wcg_ctx *ctx, int on);
 
-/* Diagnostics: tokens seen, distinct keys, tokens resolved in LDS vs global table, long keys. */
+/* Diagnostics, stats8 = {tokens, distinct keys, tokens counted in LDS, global-table operations,
+ * tokens > 15 bytes, long-key heap bytes (keys > 32 bytes; shorter long keys live in their
+ * table slot's cell), overflow, spin_fail}. */
 WCG_API int wcg_stats(wcg_ctx *ctx, uint64_t *stats8);
 
 /* FNV-1a 32 (= ihash, mapreduce.go:185-189), host side, for partition arithmetic. */

@@ -76,7 +76,7 @@ struct DevState {
     u64 lds_hits;        // tokens aggregated in LDS
     u64 global_ops;      // global-table insertions (misses + flushes)
     u64 long_tokens;     // tokens longer than 15 bytes
-    u64 arena_top;       // bytes used in the long-key arena
+    u64 arena_top;       // bytes used in the long-key arena heap (keys > 32 B; shorter keys use slot cells)
     u64 nrec;            // records produced by compaction
     u64 nlong;           // ... of which long keys (> 15 bytes)
     u32 overflow;        // table / arena full -> WCG_EFULL
