@@ -253,13 +253,14 @@ __global__ __launch_bounds__(LONG_NT) void k_long(MapArgs a, u32 nreg, int mode)
     __shared__ u64 ctag[LCACHE];
     __shared__ u64 coff[LCACHE];              // arena offset + 1 (0 = not filled)
     __shared__ u32 cslot[LCACHE], clen[LCACHE], ccnt[LCACHE];
-    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; coff[e] = 0; ccnt[e] = 0; }
-    __syncthreads();
     const u32 reg = blockIdx.x % nreg, part = blockIdx.x / nreg;
     const u32 nrec = a.llog_len[reg];
     const u64* recs = a.llog + (u64)reg * a.llog_cap;
     const u32 stride = LONG_PARTS * LONG_NT, first = part * LONG_NT;
     const u32 rounds = nrec > first ? (nrec - first + stride - 1) / stride : 0;   // workgroup-uniform
+    if (rounds == 0) return;          // ASCII text: nearly every workgroup (no barrier reached yet)
+    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; coff[e] = 0; ccnt[e] = 0; }
+    __syncthreads();
     const uint8_t* in = a.in;
     const u64 n = a.n;
     for (u32 k = 0; k < rounds; k++) {
