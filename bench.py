@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """Word-count throughput on MI355X: input GB/s (whole node) and fraction of the HBM roofline.
 
-A step = one word-count job over device-resident synthetic input (BASELINE.json config 2 per
-GPU: 1 GiB ASCII Zipf, V=1e5, s=1.0, seed 42; rank r gets the r-th GiB of the corpus): reset tables -> map kernel (tokenize +
-aggregate) -> [N > 1: export by owner, RCCL all-to-all-v, import the owned partitions, gather
-to rank 0] -> sort + format the merged "key: count\\n" output in HBM.  After the timed steps the
-merged file is checked byte for byte against the C oracle (N > 1: against the sum of every
-rank's oracle counts); a mismatch exits 3 without printing a rate.
+A step = one word-count job over device-resident synthetic input: reset tables -> map kernels
+(tokenize + aggregate) -> sort + format the merged "key: count\\n" output in HBM.
+  N = 1: BASELINE config 2 (1 GiB ASCII Zipf, V=1e5, s=1.0, seed 42), the metric's config.
+  N > 1: BASELINE config 3 (16 GiB of the same generator, seed 43, nReduce 64) split over the
+         N ranks (strong scaling): map -> export by owner (ihash % 64) % N -> RCCL all-to-all-v ->
+         owners import, sort and format their partitions -> rank 0 merges the owners' sorted runs.
+After the timed steps the merged file is checked byte for byte against the C oracle (N > 1:
+against the sum of every rank's oracle counts); a mismatch exits 3 without printing a rate.
 
   python bench.py --gpus N --steps K --warmup W
 N > 1 is launched by torch.distributed.run (one rank per GPU, backend nccl = RCCL).
@@ -33,11 +35,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30)
+    ap.add_argument("--workload", default=None,
+                    help="default: c2_ascii_zipf_1gib at N = 1 (BASELINE config 2, the metric's config); "
+                         "c3_ascii_zipf_16gib at N > 1 (BASELINE config 3: 16 GiB strong-scaled over N, nReduce 64)")
+    ap.add_argument("--bytes", type=int, default=None, help="total input bytes (default: the workload's size)")
     ap.add_argument("--nreduce", type=int, default=64)
-    ap.add_argument("--workload", default="c2_ascii_zipf_1gib")
     ap.add_argument("--cpu-sample-mib", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-end-to-end", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N > 1 path with host-staged records, ranks may share a GPU")
@@ -46,32 +51,88 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, sample_bytes):
-    """The oracle's file-based port of RunSingle (oracle/mr_port.c: Split, DoMap with one JSON
-    write(2) per token, DoReduce, Merge; wc.go's nMap=5, nReduce=3), single thread, on the first
-    `sample_bytes` of the same corpus."""
+def _timed_file_port(fn, data, fname):
     from tests import oracle_bridge as ob
-    from wcg.corpus import Generator
-    data = Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"]).bytes(sample_bytes)
     d = tempfile.mkdtemp(prefix="wcg-cpu-", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
-    fname = "cpu-sample.txt"
     try:
         with open(os.path.join(d, fname), "wb") as f:
             f.write(data)
         t0 = time.perf_counter()
-        rc = ob.run_single_files(d, fname, 5, 3)
+        rc = fn(d)
         dt = time.perf_counter() - t0
         if rc != 0:
-            raise RuntimeError("cpu baseline RunSingle failed")
+            raise RuntimeError("cpu baseline failed")
         ok = open(os.path.join(d, "mrtmp." + fname), "rb").read() == ob.merged(data)
     finally:
         for f in os.listdir(d):
             os.unlink(os.path.join(d, f))
         os.rmdir(d)
-    return {"value": round(sample_bytes / dt / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"first {sample_bytes >> 20} MiB of the same corpus, RunSingle(nMap=5, nReduce=3) "
-                      f"file-based port incl. split/intermediate/res files on tmpfs ({dt:.1f} s)",
-            "merged_equal_gpu_oracle": ok}
+    return dt, ok
+
+
+def cpu_baselines(cfg, sample_bytes):
+    """CPU baselines on this host's cores, on the first `sample_bytes` of the same corpus (the
+    reference's Go code cannot run here: no Go toolchain; these are the oracle's ports):
+      cpu_baseline           RunSingle(nMap=5, nReduce=3) file-based port (oracle/mr_port.c: Split,
+                             DoMap with one JSON write(2) per token, DoReduce, Merge), 1 thread;
+      cpu_baseline_parallel  the master/worker path's work, W worker threads taking map then
+                             reduce jobs (mrp_run_parallel, nMap = 4W, nReduce = 64);
+      cpu_restatement_all_cores  the in-memory word count (oracle/wc_oracle.c) on all cores."""
+    from tests import oracle_bridge as ob
+    from wcg.corpus import Generator
+    data = Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"]).bytes(sample_bytes)
+    fname = "cpu-sample.txt"
+    W = max(1, min(16, os.cpu_count() or 1))
+    dt1, ok1 = _timed_file_port(lambda d: ob.run_single_files(d, fname, 5, 3), data, fname)
+    dtw, okw = _timed_file_port(lambda d: ob.run_parallel_files(d, fname, 4 * W, 64, W), data, fname)
+    t0 = time.perf_counter()
+    ob.Result(data, W)
+    dtm = time.perf_counter() - t0
+    mib = sample_bytes >> 20
+    return (
+        {"value": round(sample_bytes / dt1 / 1e9, 6), "unit": "GB/s", "cores": 1, "kind": "port",
+         "sample": f"first {mib} MiB of the same corpus, RunSingle(nMap=5, nReduce=3) file-based port "
+                   f"incl. split/intermediate/res files on tmpfs ({dt1:.1f} s)", "merged_equal_gpu_oracle": ok1},
+        {"value": round(sample_bytes / dtw / 1e9, 6), "unit": "GB/s", "cores": W, "kind": "port",
+         "sample": f"first {mib} MiB, master/worker path: {W} worker threads, nMap={4 * W}, nReduce=64, "
+                   f"files on tmpfs ({dtw:.1f} s)", "merged_equal_gpu_oracle": okw},
+        {"value": round(sample_bytes / dtm / 1e9, 6), "unit": "GB/s", "cores": W, "kind": "port",
+         "sample": f"first {mib} MiB, in-memory word count (oracle/wc_oracle.c) on {W} threads ({dtm:.1f} s)"},
+    )
+
+
+def end_to_end(eng, cfg, n, reps=3):
+    """Split -> merged file on one GPU from an input file: wcg_map_file (the pinned
+    double-buffered ingest: host reads || PCIe copy || map kernels) + reduce + D2H + write of
+    mrtmp.<f>.  The file sits in tmpfs (page cache), so this is the host-read + PCIe-bound rate,
+    reported beside the device-resident metric, never as it."""
+    from wcg.corpus import Generator
+    d = tempfile.mkdtemp(prefix="wcg-e2e-", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    path = os.path.join(d, "input.txt")
+    try:
+        import torch
+        host = torch.empty(n, dtype=torch.uint8)
+        Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"]).fill_ptr(host.data_ptr(), n)
+        host.numpy().tofile(path)
+        del host
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            eng.reset()
+            mapped, size = eng.map_file(path)
+            eng.reduce()
+            out = eng.result()
+            with open(os.path.join(d, "mrtmp.input.txt"), "wb") as f:
+                f.write(out)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        return {"value": round(n / best / 1e9, 3), "unit": "GB/s", "seconds": round(best, 4),
+                "path": "input file in tmpfs -> wcg_map_file (Split + DoMap) -> reduce -> mrtmp.<f> written",
+                "mapped_bytes": mapped, "reps": reps}
+    finally:
+        for f in os.listdir(d):
+            os.unlink(os.path.join(d, f))
+        os.rmdir(d)
 
 
 def main():
@@ -85,10 +146,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("bench.py: N>1 must be launched with torch.distributed.run", file=sys.stderr)
-            sys.exit(2)
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        print("bench.py: N>1 must be launched with torch.distributed.run", file=sys.stderr)
+        sys.exit(2)
     gloo = args.dist_backend == "gloo"
     if gloo:                                  # rehearsal: ranks may share the box's GPU(s)
         local = local % torch.cuda.device_count()
@@ -100,16 +160,28 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    cfg = dict(CONFIGS[args.workload])
-    n = args.bytes_per_gpu
-    # ---- synthetic input for this rank: blocks [rank * n/BLOCK, ...) of the corpus, in HBM
+    workload = args.workload or ("c2_ascii_zipf_1gib" if world == 1 else "c3_ascii_zipf_16gib")
+    cfg = dict(CONFIGS[workload])
+    total = args.bytes or cfg["nbytes"]
+    strong = workload.startswith("c3")        # C3: 16 GiB in all, split over the N GPUs
+    if strong:
+        nblocks = (total + BLOCK - 1) // BLOCK
+        b0, b1 = nblocks * rank // world, nblocks * (rank + 1) // world
+        first_block, n = b0, min(b1 * BLOCK, total) - b0 * BLOCK
+    else:                                     # weak: every rank maps its own `total` bytes
+        first_block, n = rank * ((total + BLOCK - 1) // BLOCK), total
+    # ---- synthetic input for this rank: generator blocks [first_block, ...), line-aligned, in HBM
     host = torch.empty(n, dtype=torch.uint8).pin_memory()
     gen = Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"])
-    gen.fill_ptr(host.data_ptr(), n, first_block=rank * ((n + BLOCK - 1) // BLOCK))
+    gen.fill_ptr(host.data_ptr(), n, first_block=first_block)
     dev = host.to(f"cuda:{local}", non_blocking=False)
     torch.cuda.synchronize()
 
-    stream = torch.cuda.current_stream().cuda_stream
+    # one stream for the engine's kernels and the collectives (stream-ordered hand-overs, no host
+    # waits between export, all-to-all and import)
+    work = torch.cuda.Stream()
+    torch.cuda.set_stream(work)
+    stream = work.cuda_stream
     # table capacity: the vocabulary, but no more keys than one per 32 input bytes (C4's densest
     # slice has one distinct key per 45 bytes).  Oversized tables cost time: k_compact scans every
     # slot, and the table probes of k_agg/k_long spread over more pages (TLB) and miss the
@@ -119,10 +191,6 @@ def main():
     eng.set_stream(stream)
     eng.enable_timing(True)
     teng = wd.TorchEngine(eng, stream, host_staging=gloo)
-    root_eng = None
-    if world > 1 and rank == 0:
-        root_eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=keys_cap)
-        root_eng.set_stream(stream)
 
     def step():
         """one job; returns the device ms per phase of this rank's map (and, N = 1, reduce)"""
@@ -132,11 +200,8 @@ def main():
             eng.reduce()
             return eng.timings()[0]
         ph = eng.timings()[0]                 # taken before the shuffle's reset clears them
-        # owners need no sort of their own here: root re-sorts the union of the owners'
-        # disjoint key sets, and the merged file stays in root's HBM (fetched after timing)
-        wd.shuffle(teng, args.nreduce)
-        wd.gather_merge(teng, wd.TorchEngine(root_eng, stream, host_staging=gloo) if root_eng else None,
-                        fetch=False)
+        wd.shuffle_reduce(teng, args.nreduce)            # owners: DoReduce of their partitions
+        wd.gather_merge(teng, fetch=False)               # rank 0: k-way merge of the sorted runs
         return ph
 
     for _ in range(args.warmup):
@@ -168,8 +233,8 @@ def main():
         if world == 1:
             verified = eng.result() == ob.merged(data, 16)
         else:
-            # every rank counts its own GiB with the oracle; root sums the counts of all ranks
-            # and compares the merged file with the one the GPUs left in root's HBM
+            # every rank counts its own range with the oracle; root sums the counts of all ranks
+            # and compares the merged file the GPUs left in root's HBM
             mine = ob.merged(data, 16)
             parts = [None] * world if rank == 0 else None
             dist.gather_object(mine, parts, dst=0)
@@ -181,24 +246,25 @@ def main():
                     for line in p.splitlines():
                         k, c = line.rsplit(b": ", 1)
                         tot[k] = tot.get(k, 0) + int(c)
-                ok[0] = root_eng.result() == wc_ref.merged_output(tot)
+                ok[0] = eng.result() == wc_ref.merged_output(tot)
             dist.broadcast_object_list(ok, src=0)
             verified = ok[0]
+        del data
         if not verified:
             sys.stderr.write("bench: GPU result differs from the oracle; refusing to report a rate\n")
             sys.exit(3)
 
     if rank == 0:
         ms_step = dt / args.steps * 1e3
-        total_bytes = n * world
-        gbs = total_bytes / (dt / args.steps) / 1e9
+        all_bytes = total if strong else n * world
+        gbs = all_bytes / (dt / args.steps) / 1e9
         avg_map_ms = sum(map_ms) / len(map_ms)
         achieved = n / (avg_map_ms * 1e-3) / 1e9 if avg_map_ms > 0 else None
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("bytes_per_gpu") == n and tj.get("workload") == args.workload:
+            if tj.get("bytes_per_gpu") == n and tj.get("workload") == workload:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -211,16 +277,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (csrc/gencorpus.c; kjv12.txt absent)",
-            "config": {"workload": args.workload, "bytes_per_gpu": n, "vocab": cfg["vocab"],
+            "config": {"workload": workload, "total_bytes": all_bytes, "bytes_per_gpu": n, "vocab": cfg["vocab"],
                        "zipf_s": cfg["zipf_s"], "seed": cfg["seed"], "nreduce": args.nreduce,
                        "hbm_roofline_frac_whole_step": round(gbs / (HBM_PEAK_GBS * world), 4),
-                       "parallelism": f"{world} ranks, 1 GiB line-aligned range each",
+                       "parallelism": f"{world} ranks, one line-aligned range each",
                        "shuffle": None if world == 1 else
-                       ("gloo rehearsal, host-staged" if gloo else "RCCL all_to_all_single (counts, then records)")},
+                       ("gloo rehearsal, host-staged" if gloo else
+                        "RCCL all_to_all_single (counts, then records); owners sort; rank 0 merges the runs")},
             "roofline": {"bound": "hbm", "kernel": "wcg::k_map",
                          "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -232,8 +299,11 @@ def main():
             out["stats"] = stats
         out["phase_ms_avg"] = {k: round(sum(p[k] for p in phase_ms) / len(phase_ms), 4) for k in phase_ms[0]}
         out["verified_vs_oracle"] = verified
+        if world == 1 and not args.no_end_to_end:
+            out["end_to_end"] = end_to_end(eng, cfg, n)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample_mib << 20)
+            out["cpu_baseline"], out["cpu_baseline_parallel"], out["cpu_restatement_all_cores"] = \
+                cpu_baselines(cfg, args.cpu_sample_mib << 20)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

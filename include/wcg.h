@@ -20,6 +20,9 @@
  *   wcg_partition~ DoReduce(job=r) output bytes mrtmp.<f>-res-<r>    (mapreduce.go:264-279)
  *   wcg_export / wcg_import ~ the ihash%nReduce shuffle (mapreduce.go:214-230 + 242-263),
  *                  done as an all-to-all-v of pre-aggregated records between GPUs.
+ *   wcg_map_file ~ Split + DoMap x nMap from the input file (mapreduce.go:141-179, 193-231)
+ *   wcg_merge_runs ~ Merge of the owners' sorted DoReduce outputs  (mapreduce.go:284-321)
+ *   wcg_map_json ~ DoMap's per-occurrence JSON intermediates       (mapreduce.go:214-230)
  *
  * Conventions:
  *   - Every entry point returns int status (WCG_OK = 0); the host turns non-zero into a fatal
@@ -60,8 +63,8 @@ enum {
 };
 
 /* Open a context on HIP device `device`.
- *   max_input_bytes: largest single wcg_map() split (sizes the H2D staging buffer; 0 = none,
- *                    only wcg_map_device() is then allowed)
+ *   max_input_bytes: a hint (kept for ABI compatibility): wcg_map streams splits of any size
+ *                    through fixed pinned staging buffers; 0 is fine
  *   max_keys:        capacity in distinct keys of the device aggregation table */
 WCG_API int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx **out);
 WCG_API int wcg_close(wcg_ctx *ctx);
@@ -76,11 +79,22 @@ WCG_API int wcg_reset(wcg_ctx *ctx);
 
 /* DoMap + Map (mapreduce.go:193-231, wc.go:17-30) over one split held in host memory:
  * copy to HBM, tokenize into maximal unicode.IsLetter runs, aggregate (key, count).
- * Splits must be cut where a token cannot straddle (Split cuts at '\n'). Asynchronous. */
+ * Splits must be cut where a token cannot straddle (Split cuts at '\n').  Large splits are
+ * streamed in chunks (cut after an ASCII non-letter) through pinned double buffers, so the
+ * copy of one chunk overlaps the map of the previous one.  Returns once host_bytes has been
+ * consumed (the caller may free it); the device work is asynchronous. */
 WCG_API int wcg_map(wcg_ctx *ctx, const uint8_t *host_bytes, uint64_t n);
 
 /* Same, input already resident in device memory (n bytes at dev_bytes). Asynchronous. */
 WCG_API int wcg_map_device(wcg_ctx *ctx, const void *dev_bytes, uint64_t n);
+
+/* Split (mapreduce.go:141-179) + DoMap x nMap over a whole input file, on the GPU: the file is
+ * read by a pool of host threads into two pinned staging buffers and copied to HBM in
+ * line-aligned chunks, each copy overlapping the map kernels of the previous chunk.  Split's
+ * quirk P1 is kept: the first line that does not fit bufio.Scanner's 64 KiB buffer together with
+ * its '\n' ends the input (the reference's scan stops there silently).  *mapped_bytes = bytes
+ * counted (the whole file unless P1 cut it), *file_bytes = file size.  Asynchronous. */
+WCG_API int wcg_map_file(wcg_ctx *ctx, const char *path, uint64_t *mapped_bytes, uint64_t *file_bytes);
 
 /* DoReduce x nReduce + Merge (mapreduce.go:239-321): sort all keys bytewise on the device and
  * format the merged file "key: count\n".  Synchronous; returns key count and byte size. */
@@ -89,12 +103,33 @@ WCG_API int wcg_reduce(wcg_ctx *ctx, uint64_t *nkeys, uint64_t *nbytes);
 /* Device pointer to / host copy of the formatted output of the last wcg_reduce(). */
 WCG_API int wcg_result_device(wcg_ctx *ctx, const void **dev_ptr, uint64_t *nbytes);
 WCG_API int wcg_result_copy(wcg_ctx *ctx, uint8_t *host_out, uint64_t cap);
+/* Device-to-device copy of that output (nbytes of wcg_reduce) into dev_dst, asynchronous on the
+ * context's stream (e.g. into a collective's send buffer). */
+WCG_API int wcg_result_copy_device(wcg_ctx *ctx, void *dev_dst);
+
+/* Wait for all device work queued on the context's stream. */
+WCG_API int wcg_sync(wcg_ctx *ctx);
 
 /* Bytes of mrtmp.<f>-res-<r> (DoReduce output, mapreduce.go:264-279) for partition r of
  * nreduce, in sorted key order, copied to host_out (cap bytes).  *nbytes gets the size;
  * host_out == NULL queries the size only.  Requires a prior wcg_reduce(). */
 WCG_API int wcg_partition(wcg_ctx *ctx, uint32_t nreduce, uint32_t r, uint8_t *host_out, uint64_t cap,
                   uint64_t *nbytes);
+
+/* Every DoReduce output file at once: the nreduce -res-<r> files back to back in partition order
+ * (one formatting pass for all of them; nreduce <= 1024).  part_bytes[nreduce] gets each file's
+ * size; host_out == NULL queries the sizes only (the files stay cached on the device until the
+ * next job, so wcg_partition of any r is then a copy). */
+WCG_API int wcg_partition_all(wcg_ctx *ctx, uint32_t nreduce, uint8_t *host_out, uint64_t cap,
+                              uint64_t *part_bytes);
+
+/* DoMap's reference-exact intermediate files (mapreduce.go:214-230) for one split: for every
+ * token, in input order, the line {"Key":"tok","Value":"1"}\n in file ihash(tok) % nreduce - the
+ * bytes the reference's json.Encoder writes to mrtmp.<f>-<m>-<r>, so an unmodified CPU DoReduce
+ * can consume GPU map output.  Files back to back in partition order; part_bytes[nreduce] gets
+ * each size; host_out == NULL queries the sizes only.  Independent of the aggregation tables. */
+WCG_API int wcg_map_json(wcg_ctx *ctx, const uint8_t *host_bytes, uint64_t n, uint32_t nreduce,
+                         uint8_t *host_out, uint64_t cap, uint64_t *part_bytes);
 
 /* ---- multi-GPU shuffle (one process per GPU; the host moves the buffers with RCCL) ----
  * wcg_export: bucket the local aggregate by owner = (ihash(key) % nreduce) % nranks into a
@@ -106,6 +141,22 @@ WCG_API int wcg_partition(wcg_ctx *ctx, uint32_t nreduce, uint32_t r, uint8_t *h
 WCG_API int wcg_export(wcg_ctx *ctx, uint32_t nreduce, uint32_t nranks, const void **dev_records,
                uint64_t *counts);
 WCG_API int wcg_import(wcg_ctx *ctx, const void *dev_records, uint64_t nrecords);
+
+/* The same export in two steps, writing straight into a caller's device buffer (e.g. the send
+ * buffer of an RCCL all-to-all-v): wcg_export_count returns the units per destination rank
+ * (one host synchronisation); wcg_export_write then fills dev_dst (sum(counts) units, rank
+ * order) asynchronously on the context's stream.  wcg_import is asynchronous too: a table that
+ * filled is reported by the next wcg_reduce / wcg_export_count. */
+WCG_API int wcg_export_count(wcg_ctx *ctx, uint32_t nreduce, uint32_t nranks, uint64_t *counts);
+WCG_API int wcg_export_write(wcg_ctx *ctx, void *dev_dst);
+
+/* Merge (mapreduce.go:284-321) of sorted runs: dev_text holds nruns formatted outputs back to
+ * back (each a sorted "key: count\n" file, e.g. the wcg_reduce output of every owner rank, with
+ * disjoint keys), run r being run_bytes[r] bytes.  The runs are merged pairwise on the device
+ * (ceil(log2 nruns) merge passes, long-key ties by full bytes) into this context's result
+ * (wcg_result_device / wcg_result_copy).  Synchronous. */
+WCG_API int wcg_merge_runs(wcg_ctx *ctx, const void *dev_text, const uint64_t *run_bytes, uint32_t nruns,
+                           uint64_t *nkeys, uint64_t *nbytes);
 
 /* Per-phase device time of the last pipeline run, in milliseconds, measured with HIP events
  * on the context's stream: ms[0] map kernel (tokenize + LDS aggregation, summed over the

@@ -90,37 +90,52 @@ API void *wcgen_create(int mode, uint64_t vocab, double zipf_s, uint64_t seed) {
     uint64_t *tab = (uint64_t *)calloc(tcap, 8);                  /* index+1 of stored word */
     rng_t r; rseed(&r, seed, 0xC0FFEEull);
     uint64_t pos = 0;
-    for (uint64_t i = 0; i < vocab;) {
-        uint8_t buf[96]; uint32_t n = 0;
-        if (mode == 0) {
-            int L = 1 + poisson(&r, 4.0); if (L > 20) L = 20;
-            int cap1 = rbelow(&r, 10) == 0;
-            for (int k = 0; k < L; k++) buf[n++] = (uint8_t)((k == 0 && cap1 ? 'A' : 'a') + rbelow(&r, 26));
-        } else {
-            uint32_t pick = rbelow(&r, 100);
-            int script = pick < 40 ? 0 : pick < 50 ? 1 : pick < 60 ? 2 : pick < 70 ? 3 : pick < 85 ? 4 : pick < 95 ? 5 : 6;
-            int L = 1 + poisson(&r, script >= 4 ? 1.5 : 4.0); if (L > 12) L = 12;
-            int cap1 = rbelow(&r, 10) == 0;
-            for (int k = 0; k < L; k++) {
-                if (script == 0) buf[n++] = (uint8_t)((k == 0 && cap1 ? 'A' : 'a') + rbelow(&r, 26));
-                else {
-                    uint32_t cp = script_letter(&r, script, k == 0);
-                    if (cp == 0x3A2) cp = 0x3A3;                        /* U+03A2 is unassigned */
-                    n += (uint32_t)put_utf8(buf + n, cp);
-                }
-            }
-        }
-        uint64_t h = h64(buf, n), s = h & (tcap - 1);
+    /* Candidates come from one RNG stream whatever is accepted (a duplicate just draws the next
+     * candidate), so they are generated PF ahead of the dedupe and their table slots prefetched:
+     * the 1 GB table's random probes otherwise dominate (C4: 7.4e7 candidates). */
+    enum { PF = 64 };
+    struct cand { uint8_t buf[96]; uint32_t n; uint64_t h; } *ring = (struct cand *)malloc(PF * sizeof(struct cand));
+    #define GEN_CAND(C) do {                                                                         \
+        struct cand *c_ = (C); uint32_t n = 0; uint8_t *buf = c_->buf;                               \
+        if (mode == 0) {                                                                             \
+            int L = 1 + poisson(&r, 4.0); if (L > 20) L = 20;                                        \
+            int cap1 = rbelow(&r, 10) == 0;                                                          \
+            for (int k = 0; k < L; k++) buf[n++] = (uint8_t)((k == 0 && cap1 ? 'A' : 'a') + rbelow(&r, 26)); \
+        } else {                                                                                     \
+            uint32_t pick = rbelow(&r, 100);                                                         \
+            int script = pick < 40 ? 0 : pick < 50 ? 1 : pick < 60 ? 2 : pick < 70 ? 3 : pick < 85 ? 4 : pick < 95 ? 5 : 6; \
+            int L = 1 + poisson(&r, script >= 4 ? 1.5 : 4.0); if (L > 12) L = 12;                    \
+            int cap1 = rbelow(&r, 10) == 0;                                                          \
+            for (int k = 0; k < L; k++) {                                                            \
+                if (script == 0) buf[n++] = (uint8_t)((k == 0 && cap1 ? 'A' : 'a') + rbelow(&r, 26)); \
+                else {                                                                               \
+                    uint32_t cp = script_letter(&r, script, k == 0);                                 \
+                    if (cp == 0x3A2) cp = 0x3A3;                        /* U+03A2 is unassigned */   \
+                    n += (uint32_t)put_utf8(buf + n, cp);                                            \
+                }                                                                                    \
+            }                                                                                        \
+        }                                                                                            \
+        c_->n = n; c_->h = h64(buf, n);                                                              \
+        __builtin_prefetch(&tab[c_->h & (tcap - 1)], 1);                                             \
+    } while (0)
+    for (int k = 0; k < PF; k++) GEN_CAND(&ring[k]);
+    for (uint64_t i = 0, head = 0; i < vocab; head = (head + 1) % PF) {
+        struct cand *c = &ring[head];
+        uint64_t s = c->h & (tcap - 1);
         int dup = 0;
         while (tab[s]) {
             uint64_t j = tab[s] - 1;
-            if (g->len[j] == n && memcmp(g->words + g->off[j], buf, n) == 0) { dup = 1; break; }
+            if (g->len[j] == c->n && memcmp(g->words + g->off[j], c->buf, c->n) == 0) { dup = 1; break; }
             s = (s + 1) & (tcap - 1);
         }
-        if (dup) continue;
-        tab[s] = i + 1;
-        memcpy(g->words + pos, buf, n); g->off[i] = pos; g->len[i] = n; pos += n; i++;
+        if (!dup) {
+            tab[s] = i + 1;
+            memcpy(g->words + pos, c->buf, c->n); g->off[i] = pos; g->len[i] = c->n; pos += c->n; i++;
+        }
+        GEN_CAND(c);                     /* the candidate PF places later in the stream */
     }
+    #undef GEN_CAND
+    free(ring);
     free(tab);
     /* Vose alias table for Zipf(s) over rank 1..V */
     double *p = (double *)malloc(vocab * sizeof(double)), sum = 0;

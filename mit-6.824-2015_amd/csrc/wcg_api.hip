@@ -1,16 +1,22 @@
 // wcg_api.hip - C ABI of libwcg.so (declared in include/wcg.h).
 //
-// One context = one GPU's share of a word-count job.  Device memory is allocated once at
-// wcg_open and sized for 288 GB HBM parts: the aggregation tables, the record buffers for
-// the sort and the formatted output all stay resident, so a job is a fixed sequence of
-// launches on one stream.
+// One context = one GPU's share of a word-count job.  Device memory is allocated at wcg_open
+// (tables, records) or on first need (sort items, staging), sized for 288 GB HBM parts: the
+// aggregation tables, the record buffers for the sort and the formatted output all stay
+// resident, so a job is a fixed sequence of launches on one stream.
 #include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/wcg.h"
@@ -18,6 +24,7 @@
 #include "wcg_map.h"
 #include "wcg_agg.h"
 #include "wcg_reduce.h"
+#include "wcg_ingest.h"
 
 using namespace wcg;
 
@@ -27,25 +34,47 @@ struct wcg_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     u64 max_input = 0, max_keys = 0;
-    uint8_t* d_in = nullptr;
     GEntry* gtab = nullptr; u64 gslots = 0;
     GEntry* ltab = nullptr; u64 lslots = 0;
     uint8_t* arena = nullptr; u64 arena_cap = 0;
     DevState* st = nullptr;
     DevState* h_st = nullptr;                 // pinned mirror
     Rec* recA = nullptr; Rec* recB = nullptr; u64 rec_cap = 0;
-    Rec* sorted = nullptr;
-    u64* lens = nullptr;
+    Rec* sorted = nullptr;                    // recB, or a merge pass's last output
+    u64* lens = nullptr; u64 lens_cap = 0;    // per-tile sums of the formatter
     u64* d_scalar = nullptr;                  // scan totals
-    u64* h_scalar = nullptr;                  // pinned mirror of d_scalar[0]
+    u64* h_scalar = nullptr;                  // pinned scratch (64 u64)
     uint8_t* d_out = nullptr; u64 out_cap = 0; u64 out_len = 0;
-    uint8_t* d_part = nullptr; u64 part_cap = 0;
     u64 nrec = 0;
     bool compacted = false, reduced = false;
+    // sort (wcg_sort.h)
+    Rec* smp = nullptr; u64 smp_cap = 0;      // 2 x sample records (merge ping-pong)
+    u32* bid = nullptr; u64 bid_cap = 0;
+    u32* hist = nullptr; u64 hist_cap = 0;    // [B][G] bucket counts / partition counts
+    u64* spart = nullptr; u64 spart_cap = 0;  // multi-block scan partials
+    uint4* ikey = nullptr; u32* iidx = nullptr; u64 item_cap = 0;   // 2n items
+    u64* groups = nullptr; u64 groups_cap = 0;
+    // every -res-<r> (wcg_partition_all): valid for part_R while reduced
+    u32 part_R = 0;
+    std::vector<u64> part_bytes;
+    u32* pid = nullptr; u64 pid_cap = 0;
+    u64* d_partb = nullptr; u64 partb_cap = 0;
+    uint8_t* d_part = nullptr; u64 part_cap = 0;
     // export
-    u32* owner = nullptr;
+    u32* owner = nullptr; u64 owner_cap = 0;
     u64* d_per_rank = nullptr;                // [2 * 1024]: counts, cursors
+    u64* h_cur = nullptr;                     // pinned cursors (1024)
+    bool exp_ready = false; u32 exp_nranks = 0; u64 exp_total = 0;
     Rec* exp_buf = nullptr; u64 exp_cap = 0;
+    // merge of formatted runs
+    u64* nlpos = nullptr; u64 nlpos_cap = 0;
+    u64* d_rb = nullptr; u64* d_b0 = nullptr; u64 rb_cap = 0;
+    u64* h_rb = nullptr; u64 h_rb_cap = 0;    // pinned run bounds
+    // per-occurrence JSON map output (wcg_map_json)
+    uint8_t* d_jin = nullptr; u64 jin_cap = 0;
+    uint8_t* d_jout = nullptr; u64 jout_cap = 0;
+    u64* jhist = nullptr; u64 jhist_cap = 0;
+    std::vector<u64> jparts;
     // miss log (k_map -> k_agg)
     u64* pool = nullptr; u64 pool_bytes = 0;
     u32* region_len = nullptr; u64 region_len_cap = 0;
@@ -54,6 +83,15 @@ struct wcg_ctx {
     u64* llog = nullptr; u64 llog_cap = 0;
     u32* llog_len = nullptr; u64 llog_len_cap = 0;
     u32 nbuckets = 64;
+    // ingest (wcg_ingest.h): two pinned staging buffers, two device buffers, a reader pool
+    u64 chunk = 64ull << 20;
+    uint8_t* hb[2] = {nullptr, nullptr};
+    uint8_t* db[2] = {nullptr, nullptr};
+    uint8_t* dbig = nullptr; u64 dbig_cap = 0;
+    hipEvent_t ev_copied[2] = {}, ev_mapped[2] = {};
+    hipStream_t copy_stream = nullptr;
+    std::unique_ptr<TaskPool> readers;
+    u64 ingest_bytes = 0;                     // bytes mapped by the last wcg_map / wcg_map_file
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -76,11 +114,19 @@ namespace {
         }                                                                                   \
     } while (0)
 
+#define RC(call)                                                                            \
+    do {                                                                                    \
+        int rc_ = (call);                                                                   \
+        if (rc_) return rc_;                                                                \
+    } while (0)
+
 u64 next_pow2(u64 x) {
     u64 p = 1;
     while (p < x) p <<= 1;
     return p;
 }
+
+u64 cdiv(u64 a, u64 b) { return (a + b - 1) / b; }
 
 int set_dev(wcg_ctx* c) {
     hipError_t e = hipSetDevice(c->device);
@@ -107,6 +153,10 @@ hipEvent_t take_event(wcg_ctx* c) {
 int check_status(wcg_ctx* c) {
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_st->bad_input) {
+        c->err = "malformed record units were imported (wcg_import of a buffer wcg_export did not write)";
+        return WCG_EINVAL;
+    }
     if (c->h_st->overflow || c->h_st->spin_fail) {
         char buf[256];
         snprintf(buf, sizeof buf,
@@ -119,72 +169,328 @@ int check_status(wcg_ctx* c) {
     return WCG_OK;
 }
 
-int ensure(wcg_ctx* c, uint8_t** p, u64* cap, u64 need) {
-    if (need <= *cap) return WCG_OK;
-    u64 nc = std::max<u64>(need + need / 4, 1 << 20);
-    if (*p) HIPCHK(c, hipFree(*p));
+// device buffer of at least `need` elements of T (contents are not kept); waits for the stream
+// before freeing a buffer that in-flight work may still use
+template <typename T>
+int ensure(wcg_ctx* c, T** p, u64* cap, u64 need) {
+    if (need <= *cap && *p) return WCG_OK;
+    u64 nc = std::max<u64>(need + need / 4, (1u << 20) / sizeof(T));
+    if (*p) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(*p));
+    }
     *p = nullptr;
     *cap = 0;
-    HIPCHK(c, hipMalloc(p, nc));
+    HIPCHK(c, hipMalloc((void**)p, nc * sizeof(T)));
     *cap = nc;
     return WCG_OK;
 }
 
+// record buffers (compaction output, sort / merge ping-pong) for n records; the contents of
+// recA are kept (records may already be in it)
+int ensure_recs(wcg_ctx* c, u64 n) {
+    if (n <= c->rec_cap) return WCG_OK;
+    const u64 nc = n + n / 4;
+    Rec *a = nullptr, *b = nullptr;
+    HIPCHK(c, hipMalloc(&a, nc * sizeof(Rec)));
+    HIPCHK(c, hipMalloc(&b, nc * sizeof(Rec)));
+    HIPCHK(c, hipMemcpyAsync(a, c->recA, c->rec_cap * sizeof(Rec), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(c->recA));
+    HIPCHK(c, hipFree(c->recB));
+    c->recA = a; c->recB = b; c->rec_cap = nc;
+    return WCG_OK;
+}
+
+// tables -> recA; the record buffers start at max_keys records and grow (then the compaction
+// runs again) when the tables hold more keys than that
 int compact(wcg_ctx* c) {
     if (c->compacted) return WCG_OK;
-    HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));   // nrec, nlong
-    if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
-    u64 total = c->gslots + c->lslots;
-    k_compact<<<(unsigned)((total + CP_NT * CP_IPT - 1) / (CP_NT * CP_IPT)), CP_NT, 0, c->stream>>>(
-        c->gtab, c->gslots, c->ltab, c->lslots, c->arena, c->recA, c->st);
-    HIPCHK(c, hipGetLastError());
-    if (c->timing) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
-    int rc = check_status(c);
-    if (rc) return rc;
-    c->nrec = c->h_st->nrec;
+    for (int pass = 0; pass < 2; pass++) {
+        HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));   // nrec, nlong
+        if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
+        const u64 total = c->gslots + c->lslots;
+        k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
+            c->gtab, c->gslots, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st);
+        HIPCHK(c, hipGetLastError());
+        if (c->timing) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
+        RC(check_status(c));
+        c->nrec = c->h_st->nrec;
+        if (c->nrec <= c->rec_cap) break;
+        RC(ensure_recs(c, c->nrec));
+    }
     c->compacted = true;
     return WCG_OK;
 }
 
-// merge sort of recA[0:nrec) by the 128-bit prefix (no host round trip); result in c->sorted
-int sort_records(wcg_ctx* c) {
-    const u64 n = c->nrec;
-    c->sorted = c->recA;
-    if (n <= 1) return WCG_OK;
-    Rec* src = c->recA;
-    Rec* dst = c->recB;
-    k_tile_sort<<<(unsigned)((n + TS_TILE - 1) / TS_TILE), TS_NT, 0, c->stream>>>(src, dst, n);
-    HIPCHK(c, hipGetLastError());
-    std::swap(src, dst);
-    for (u64 w = TS_TILE; w < n; w *= 2) {
-        k_merge<<<(unsigned)((n + MG_CHUNK - 1) / MG_CHUNK), MG_NT, 0, c->stream>>>(src, dst, n, w);
-        HIPCHK(c, hipGetLastError());
-        std::swap(src, dst);
-    }
-    c->sorted = src;
-    // long keys sharing a 16-byte prefix (needs two long keys at least)
-    if (c->h_st->nlong >= 2)
-        k_tie_fix<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(c->sorted, n, c->arena);
+// WCG_DEBUG=1: synchronise and report after each stage of the rarely used paths (diagnostics)
+int dbg(wcg_ctx* c, const char* what) {
+    static const bool on = getenv("WCG_DEBUG") != nullptr;
+    if (!on) return WCG_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    fprintf(stderr, "wcg: %s done\n", what);
+    return WCG_OK;
+}
+
+// exclusive scan of m u32 in place (multi-block)
+int scan_u32(wcg_ctx* c, u32* v, u64 m) {
+    const u64 nb = cdiv(m, SC_SEG);
+    RC(ensure(c, &c->spart, &c->spart_cap, nb + 1));
+    k_scan_part<<<(unsigned)nb, SC_NT, 0, c->stream>>>(v, m, c->spart);
+    k_scan_u64<<<1, 1024, 0, c->stream>>>(c->spart, nb, nullptr);
+    k_scan_apply<<<(unsigned)nb, SC_NT, 0, c->stream>>>(v, m, c->spart);
     HIPCHK(c, hipGetLastError());
     return WCG_OK;
 }
 
-// format sorted records into a device buffer sized by an upper bound (so nothing waits for
-// the host before the write); one synchronisation at the end returns the exact size
-int format(wcg_ctx* c, int fmt, u32 nreduce, u32 part, uint8_t** dbuf, u64* cap, u64* nbytes) {
+// stable merge sort of n records (tile sort + passes); returns the buffer holding the result
+int merge_sort(wcg_ctx* c, Rec* a, Rec* b, u64 n, Rec** result) {
+    k_tile_sort<<<(unsigned)cdiv(n, TS_TILE), TS_NT, 0, c->stream>>>(a, b, n);
+    HIPCHK(c, hipGetLastError());
+    Rec *src = b, *dst = a;
+    for (u64 w = TS_TILE; w < n; w *= 2) {
+        k_merge<<<(unsigned)cdiv(n, MG_CHUNK), MG_NT, 0, c->stream>>>(src, dst, n, w);
+        HIPCHK(c, hipGetLastError());
+        std::swap(src, dst);
+    }
+    *result = src;
+    return WCG_OK;
+}
+
+// items (2n): ikey and iidx are allocated together
+int ensure_items(wcg_ctx* c, u64 n2) {
+    if (n2 <= c->item_cap && c->ikey && c->iidx) return WCG_OK;
+    if (c->ikey || c->iidx) HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->ikey) HIPCHK(c, hipFree(c->ikey));
+    if (c->iidx) HIPCHK(c, hipFree(c->iidx));
+    c->ikey = nullptr; c->iidx = nullptr; c->item_cap = 0;
+    const u64 nc = std::max<u64>(n2 + n2 / 4, 1 << 16);
+    HIPCHK(c, hipMalloc(&c->ikey, nc * sizeof(uint4)));
+    HIPCHK(c, hipMalloc(&c->iidx, nc * sizeof(u32)));
+    c->item_cap = nc;
+    return WCG_OK;
+}
+
+// long keys sharing a 16-byte prefix in r[0:n): ordered by their full bytes (key bytes at
+// `base`); `tmp` is a free record buffer of n records
+int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp) {
+    if (n < 2) return WCG_OK;
+    RC(ensure(c, &c->groups, &c->groups_cap, n / 2 + 2));
+    RC(ensure_items(c, 2 * n));
+    HIPCHK(c, hipMemsetAsync(c->groups, 0, sizeof(u64), c->stream));
+    k_tie_mark<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(r, n, c->groups + 1, c->groups);
+    TieArgs t;
+    t.r = r; t.n = n; t.base = base; t.groups = c->groups + 1; t.ngroups = c->groups;
+    t.tmp = tmp; t.sc_key = c->ikey; t.sc_pos = c->iidx;
+    k_tie_sort<<<(unsigned)c->ncu, TG_NT, 0, c->stream>>>(t);
+    HIPCHK(c, hipGetLastError());
+    return WCG_OK;
+}
+
+// sample sort of recA[0:nrec) into recB (wcg_sort.h), then the tie groups
+int sort_records(wcg_ctx* c) {
     const u64 n = c->nrec;
+    c->sorted = c->recB;
+    if (n == 0) return WCG_OK;
+    if (n == 1) {
+        HIPCHK(c, hipMemcpyAsync(c->recB, c->recA, sizeof(Rec), hipMemcpyDeviceToDevice, c->stream));
+        return WCG_OK;
+    }
+    if (n >= (1ull << 32)) { c->err = "sort: more than 2^32 distinct keys"; return WCG_EINVAL; }
+    // WCG_SORT_TARGET (tests only): records per bucket; above SS_CAP it forces the global path
+    const char* tenv = getenv("WCG_SORT_TARGET");
+    const u64 target_env = tenv ? strtoull(tenv, nullptr, 10) : 0;
+    u64 target = target_env ? target_env : SS_TARGET;
+    target = std::max<u64>(target, cdiv(n, SS_MAXB));
+    SortArgs a;
+    a.rec = c->recA; a.n = n; a.out = c->recB;
+    a.B = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, target), SS_MAXB));
+    a.S = a.B > 1 ? std::min<u64>(n, (u64)a.B * SS_OVS) : 0;
+    a.smp = nullptr;
+    if (a.B > 1) {
+        RC(ensure(c, &c->smp, &c->smp_cap, 2 * a.S));
+        k_ss_sample<<<(unsigned)cdiv(a.S, 256), 256, 0, c->stream>>>(a, c->smp);
+        HIPCHK(c, hipGetLastError());
+        Rec* s = nullptr;
+        RC(merge_sort(c, c->smp, c->smp + a.S, a.S, &s));
+        a.smp = s;
+    }
+    a.G = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, 4096), (u64)c->ncu));
+    RC(ensure(c, &c->bid, &c->bid_cap, n));
+    RC(ensure(c, &c->hist, &c->hist_cap, (u64)a.B * a.G));
+    RC(ensure_items(c, 2 * n));
+    a.bid = c->bid; a.hist = c->hist;
+    a.ikey = c->ikey; a.iidx = c->iidx; a.ikey2 = c->ikey + n; a.iidx2 = c->iidx + n;
+    k_ss_hist<<<a.G, SS_NT, 0, c->stream>>>(a);
+    HIPCHK(c, hipGetLastError());
+    RC(scan_u32(c, c->hist, (u64)a.B * a.G));
+    k_ss_scatter<<<a.G, SS_NT, 0, c->stream>>>(a);
+    k_ss_bucket<<<a.B, SB_NT, 0, c->stream>>>(a);
+    HIPCHK(c, hipGetLastError());
+    if (c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA));
+    c->compacted = false;          // recA was scratch for the ties
+    return WCG_OK;
+}
+
+// format records r[0:n) (key bytes of long records at `base`) into *dbuf, `bound` bytes at most;
+// one synchronisation at the end returns the exact size
+int format(wcg_ctx* c, const Rec* r, u64 n, const uint8_t* base, int fmt, u32 nreduce, u32 part, u64 bound,
+           uint8_t** dbuf, u64* cap, u64* nbytes) {
     if (n == 0) { *nbytes = 0; return WCG_OK; }
-    const u64 bound = n * (LONG_CELL + JSON_FIXED + 20) + c->h_st->arena_top + 64;   // keys <= 32 B + heap keys
-    int rc = ensure(c, dbuf, cap, bound);
-    if (rc) return rc;
-    const unsigned nt = (unsigned)((n + FM_TILE - 1) / FM_TILE);
-    k_fmt_sum<<<nt, FM_NT, 0, c->stream>>>(c->sorted, n, fmt, nreduce, part, c->arena, c->lens);
+    RC(ensure(c, dbuf, cap, bound + 64));
+    const u64 nt = cdiv(n, FM_TILE);
+    RC(ensure(c, &c->lens, &c->lens_cap, nt + 1));
+    k_fmt_sum<<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, fmt, nreduce, part, base, c->lens);
     k_scan_u64<<<1, 1024, 0, c->stream>>>(c->lens, nt, c->d_scalar);
-    k_fmt_write<<<nt, FM_NT, 0, c->stream>>>(c->sorted, n, fmt, nreduce, part, c->arena, c->lens, *dbuf);
+    k_fmt_write<<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, fmt, nreduce, part, base, c->lens, *dbuf);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *nbytes = *c->h_scalar;
+    return WCG_OK;
+}
+
+u64 merged_bound(wcg_ctx* c, u64 n, bool json) {
+    // inline keys <= 15 bytes; long keys <= 32 bytes in their cell, longer ones on the heap
+    return n * (LONG_CELL + (json ? JSON_FIXED : 3) + 20) + c->h_st->arena_top + 64;
+}
+
+// every -res-<r> for nreduce R, back to back in c->d_part (cached until the next job)
+int partition_all(wcg_ctx* c, u32 R) {
+    if (c->part_R == R) return WCG_OK;
+    const u64 n = c->nrec;
+    c->part_bytes.assign(R, 0);
+    if (n == 0) { c->part_R = R; return WCG_OK; }
+    if (R > PT_MAXR) { c->err = "wcg_partition: nreduce above 1024"; return WCG_EINVAL; }
+    const u64 T = cdiv(n, PT_TILE);
+    RC(ensure(c, &c->pid, &c->pid_cap, n));
+    RC(ensure(c, &c->hist, &c->hist_cap, (u64)R * T));
+    RC(ensure(c, &c->d_partb, &c->partb_cap, R));
+    HIPCHK(c, hipMemsetAsync(c->d_partb, 0, R * sizeof(u64), c->stream));
+    k_part_hist<<<(unsigned)T, PT_NT, 0, c->stream>>>(c->sorted, n, R, c->arena, c->pid, c->hist, c->d_partb);
+    HIPCHK(c, hipGetLastError());
+    RC(scan_u32(c, c->hist, (u64)R * T));
+    Rec* grouped = c->sorted == c->recA ? c->recB : c->recA;
+    k_part_scatter<<<(unsigned)T, PT_NT, 0, c->stream>>>(c->sorted, n, R, c->pid, c->hist, grouped);
+    HIPCHK(c, hipGetLastError());
+    c->compacted = false;
+    HIPCHK(c, hipMemcpyAsync(c->part_bytes.data(), c->d_partb, R * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    u64 total = 0;
+    for (u32 r = 0; r < R; r++) total += c->part_bytes[r];
+    u64 got = 0;
+    RC(format(c, grouped, n, c->arena, FMT_JSON_ALL, 1, 0, total, &c->d_part, &c->part_cap, &got));
+    if (got != total) { c->err = "wcg_partition: formatted size mismatch"; return WCG_EHIP; }
+    c->part_R = R;
+    return WCG_OK;
+}
+
+// ---------------------------------------------------------------- ingest
+int ingest_init(wcg_ctx* c) {
+    if (c->hb[0]) return WCG_OK;
+    for (int i = 0; i < 2; i++) {
+        HIPCHK(c, hipHostMalloc(&c->hb[i], c->chunk + SCAN_MAX_LINE + 64, hipHostMallocDefault));
+        HIPCHK(c, hipMalloc(&c->db[i], c->chunk + SCAN_MAX_LINE + 64));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_mapped[i], hipEventDisableTiming));
+    }
+    HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    unsigned hw = std::thread::hardware_concurrency();
+    c->readers.reset(new TaskPool((int)std::max(1u, std::min(16u, hw ? hw : 1u))));
+    return WCG_OK;
+}
+
+// a byte after which no rune and no token continues: an ASCII byte that is not a letter
+inline bool safe_cut_byte(uint8_t b) { return b < 0x80 && ((b | 0x20) - 'a') >= 26u; }
+
+// Stream `size` bytes from `read(dst, off, len)` through the staging buffers into the map
+// kernels.  split_mode: Split's semantics (cut after '\n', a line of 64 KiB or more ends the
+// input: quirk P1); otherwise DoMap's (every byte is mapped; chunks are cut after any ASCII
+// non-letter, so no token or rune straddles a cut).  *mapped = bytes mapped.
+int ingest(wcg_ctx* c, u64 size, const std::function<void(uint8_t*, u64, u64)>& read, bool split_mode, u64* mapped) {
+    *mapped = 0;
+    if (size == 0) return WCG_OK;
+    RC(ingest_init(c));
+    TaskPool& pool = *c->readers;
+    u64 fo = 0, carry = 0, cut_prev = 0;
+    int slot = 0;
+    std::vector<SliceLines> sl(pool.size());
+    while (true) {
+        HIPCHK(c, hipEventSynchronize(c->ev_copied[slot]));          // staging slot free
+        uint8_t* h = c->hb[slot];
+        if (carry) memmove(h, c->hb[slot ^ 1] + cut_prev, carry);
+        // the staging buffers hold chunk + SCAN_MAX_LINE bytes (a split-mode carry is < 64 KiB; a
+        // DoMap-mode carry can be larger, then less is read)
+        const u64 want = std::min<u64>(c->chunk + SCAN_MAX_LINE - carry, size - fo);
+        const int T = want >= (4ull << 20) ? pool.size() : 1;
+        if (T == 1) {
+            read(h + carry, fo, want);
+            if (split_mode) sl[0] = scan_slice(h, (int64_t)carry, (int64_t)(carry + want));
+        } else {
+            pool.run(T, [&](int t) {
+                const u64 a = carry + want * t / T, b = carry + want * (t + 1) / T;
+                read(h + a, fo + (a - carry), b - a);
+                if (split_mode) sl[t] = scan_slice(h, (int64_t)a, (int64_t)b);
+            });
+        }
+        const u64 len = carry + want;
+        fo += want;
+        const bool eof = fo == size;
+        bool stop = eof;
+        u64 cut;
+        if (split_mode) {
+            // the carry is one partial line (no '\n'); lines start at 0 and after every '\n'
+            int64_t prev = -1, bad = -1;
+            for (int t = 0; t < T && bad < 0; t++) {
+                if (sl[t].first < 0) continue;
+                if (sl[t].first - (prev + 1) >= (int64_t)SCAN_MAX_LINE) { bad = prev + 1; break; }
+                if (sl[t].bad >= 0) { bad = sl[t].bad; break; }
+                prev = sl[t].last;
+            }
+            if (bad < 0 && (int64_t)len - (prev + 1) >= (int64_t)SCAN_MAX_LINE) bad = prev + 1;
+            if (bad >= 0) { cut = (u64)bad; stop = true; }
+            else cut = eof ? len : (u64)(prev + 1);
+        } else if (eof) {
+            cut = len;
+        } else {
+            cut = 0;
+            for (u64 i = len; i > 0; i--)
+                if (safe_cut_byte(h[i - 1])) { cut = i; break; }
+            if (cut == 0) {
+                // a token or rune run longer than the chunk: map the whole rest in one call from
+                // a device buffer of its size (pathological input, e.g. 64 MiB of letters)
+                const u64 rest = len + (size - fo);
+                RC(ensure(c, &c->dbig, &c->dbig_cap, rest + 64));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                HIPCHK(c, hipMemcpy(c->dbig, h, len, hipMemcpyHostToDevice));
+                u64 done = len;
+                while (fo < size) {
+                    const u64 w = std::min<u64>(c->chunk, size - fo);
+                    read(h, fo, w);
+                    HIPCHK(c, hipMemcpy(c->dbig + done, h, w, hipMemcpyHostToDevice));
+                    fo += w;
+                    done += w;
+                }
+                RC(wcg_map_device(c, c->dbig, done));
+                *mapped += done;
+                return WCG_OK;
+            }
+        }
+        if (cut > 0) {
+            // the copy stream waits until the device slot's previous map is done
+            HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->ev_mapped[slot], 0));
+            HIPCHK(c, hipMemcpyAsync(c->db[slot], h, cut, hipMemcpyHostToDevice, c->copy_stream));
+            HIPCHK(c, hipEventRecord(c->ev_copied[slot], c->copy_stream));
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_copied[slot], 0));
+            RC(wcg_map_device(c, c->db[slot], cut));
+            HIPCHK(c, hipEventRecord(c->ev_mapped[slot], c->stream));
+            *mapped += cut;
+        }
+        if (stop) break;
+        carry = len - cut;
+        cut_prev = cut;
+        slot ^= 1;
+    }
     return WCG_OK;
 }
 
@@ -220,23 +526,19 @@ int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx** 
     c->gslots = next_pow2(2 * c->max_keys);
     c->lslots = std::max<u64>(next_pow2(c->gslots / 4), 4096);
     c->arena_cap = std::max<u64>(64ull << 20, c->lslots * 32);   // heap part (after the slot cells)
-    c->rec_cap = c->gslots / 2 + c->lslots / 2 + 16;
-    if (c->max_input) HIPCHK(c, hipMalloc(&c->d_in, c->max_input + 64));
     HIPCHK(c, hipMalloc(&c->gtab, c->gslots * sizeof(GEntry)));
     HIPCHK(c, hipMalloc(&c->ltab, c->lslots * sizeof(GEntry)));
     HIPCHK(c, hipMalloc(&c->arena, c->lslots * LONG_CELL + c->arena_cap + 64));
     HIPCHK(c, hipMalloc(&c->st, sizeof(DevState)));
     HIPCHK(c, hipHostMalloc(&c->h_st, sizeof(DevState), hipHostMallocDefault));
     // records: compaction output is bounded by the number of occupied slots
-    u64 recs = c->gslots + c->lslots;
-    c->rec_cap = recs;
-    HIPCHK(c, hipMalloc(&c->recA, recs * sizeof(Rec)));
-    HIPCHK(c, hipMalloc(&c->recB, recs * sizeof(Rec)));
-    HIPCHK(c, hipMalloc(&c->lens, recs * sizeof(u64)));
-    HIPCHK(c, hipMalloc(&c->d_scalar, 64));
-    HIPCHK(c, hipHostMalloc(&c->h_scalar, 64, hipHostMallocDefault));
-    HIPCHK(c, hipMalloc(&c->owner, recs * sizeof(u32)));
-    HIPCHK(c, hipMalloc(&c->d_per_rank, 2 * 1024 * sizeof(u64)));
+    c->rec_cap = c->max_keys + 65536;
+    HIPCHK(c, hipMalloc(&c->recA, c->rec_cap * sizeof(Rec)));
+    HIPCHK(c, hipMalloc(&c->recB, c->rec_cap * sizeof(Rec)));
+    HIPCHK(c, hipMalloc(&c->d_scalar, 64 * sizeof(u64)));
+    HIPCHK(c, hipHostMalloc(&c->h_scalar, 64 * sizeof(u64), hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc(&c->h_cur, EX_MAX_RANKS * sizeof(u64), hipHostMallocDefault));
+    HIPCHK(c, hipMalloc(&c->d_per_rank, 2 * EX_MAX_RANKS * sizeof(u64)));
     return wcg_reset(c);
 }
 
@@ -244,13 +546,25 @@ int wcg_close(wcg_ctx* c) {
     if (!c) return WCG_EINVAL;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    c->readers.reset();
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    void* bufs[] = {c->d_in, c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens,
-                    c->d_scalar, c->d_out, c->d_part, c->owner, c->d_per_rank, c->exp_buf,
-                    c->pool, c->region_len, c->wg_stats, c->llog, c->llog_len};
+    for (int i = 0; i < 2; i++) {
+        if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
+        if (c->ev_mapped[i]) (void)hipEventDestroy(c->ev_mapped[i]);
+        if (c->hb[i]) (void)hipHostFree(c->hb[i]);
+        if (c->db[i]) (void)hipFree(c->db[i]);
+    }
+    void* bufs[] = {c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens, c->d_scalar, c->d_out,
+                    c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
+                    c->llog, c->llog_len, c->smp, c->bid, c->hist, c->spart, c->ikey, c->iidx, c->groups,
+                    c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
+    if (c->h_cur) (void)hipHostFree(c->h_cur);
+    if (c->h_rb) (void)hipHostFree(c->h_rb);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return WCG_OK;
@@ -276,6 +590,8 @@ int wcg_reset(wcg_ctx* c) {
     HIPCHK(c, hipMemsetAsync(c->ltab, 0, c->lslots * sizeof(GEntry), c->stream));
     HIPCHK(c, hipMemsetAsync(c->st, 0, sizeof(DevState), c->stream));
     c->compacted = c->reduced = false;
+    c->exp_ready = false;
+    c->part_R = 0;
     c->nrec = 0;
     c->out_len = 0;
     c->map_ev.clear();
@@ -298,7 +614,9 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     a.ntiles = (n + MAP_STEP - 1) / MAP_STEP;      // 992-byte wave steps (1 KiB windows)
     // one workgroup per CU (LDS-bound); steps are dealt chip-wide inside the kernel
     u64 grid = std::min<u64>((u64)c->ncu, (a.ntiles + MAP_WAVES - 1) / MAP_WAVES);
-    a.tiles_per_wg = (a.ntiles + grid - 1) / grid;          // steps per workgroup (sizing only)
+    // steps per workgroup (sizing only): wave w of workgroup g takes steps g*16 + w + k*G*16, so
+    // a workgroup runs at most MAP_WAVES * ceil(ntiles / (G * MAP_WAVES)) of them
+    a.tiles_per_wg = MAP_WAVES * ((a.ntiles + grid * MAP_WAVES - 1) / (grid * MAP_WAVES));
     a.gtab = c->gtab; a.gmask = c->gslots - 1;
     a.ltab = c->ltab; a.lmask = c->lslots - 1;
     a.arena = c->arena; a.arena_cap = c->arena_cap;
@@ -335,9 +653,10 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         HIPCHK(c, hipMalloc(&c->wg_stats, grid * 4 * sizeof(u64)));
         c->wg_stats_cap = grid;
     }
-    // long-token log: a token > 15 bytes takes >= 17 input bytes, so a 992-byte step logs at
-    // most 59 of them; 60 records per step bound a workgroup's region
-    a.llog_cap = (u32)std::min<u64>((u64)a.tiles_per_wg * 60 + 64, 0xFFFFFFFFull);
+    // long-token log: sized for LLOG_PER_STEP records per step on average (C4 text logs ~5.3);
+    // tokens past a full region are counted inline by k_map (long_token: exact, slower), so an
+    // adversarial input costs time, never memory or an error
+    a.llog_cap = (u32)std::min<u64>((u64)a.tiles_per_wg * LLOG_PER_STEP + 64, 0xFFFFFFFFull);
     const u64 lneed = grid * (u64)a.llog_cap * sizeof(u64);
     if (lneed > c->llog_cap) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -396,20 +715,43 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     }
     c->map_launches++;
     c->compacted = c->reduced = false;
+    c->exp_ready = false;
+    c->part_R = 0;
     return WCG_OK;
 }
 
 int wcg_map(wcg_ctx* c, const uint8_t* host_bytes, uint64_t n) {
     if (!c) return WCG_EINVAL;
     if (n == 0) return WCG_OK;
-    if (!c->d_in || n > c->max_input) { c->err = "wcg_map: split larger than max_input_bytes"; return WCG_EINVAL; }
+    if (!host_bytes) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->d_in, host_bytes, n, hipMemcpyHostToDevice, c->stream));
-    rc = wcg_map_device(c, c->d_in, n);
+    return ingest(c, n, [&](uint8_t* dst, u64 off, u64 len) { memcpy(dst, host_bytes + off, len); }, false,
+                  &c->ingest_bytes);
+}
+
+int wcg_map_file(wcg_ctx* c, const char* path, uint64_t* mapped_bytes, uint64_t* file_bytes) {
+    if (!c || !path) return WCG_EINVAL;
+    int rc = set_dev(c);
     if (rc) return rc;
-    // the staging buffer is reused by the next call: finish this one first
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) { c->err = std::string("wcg_map_file: open ") + path + ": " + strerror(errno); return WCG_EINVAL; }
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) { close(fd); c->err = "wcg_map_file: stat failed"; return WCG_EINVAL; }
+    const u64 size = (u64)sb.st_size;
+    bool ioerr = false;
+    rc = ingest(c, size, [&](uint8_t* dst, u64 off, u64 len) {
+        while (len) {
+            const ssize_t r = pread(fd, dst, len, (off_t)off);
+            if (r <= 0) { ioerr = true; memset(dst, '\n', len); return; }
+            dst += r; off += (u64)r; len -= (u64)r;
+        }
+    }, true, &c->ingest_bytes);
+    close(fd);
+    if (rc) return rc;
+    if (ioerr) { c->err = "wcg_map_file: read error"; return WCG_EHIP; }
+    if (mapped_bytes) *mapped_bytes = c->ingest_bytes;
+    if (file_bytes) *file_bytes = size;
     return WCG_OK;
 }
 
@@ -417,18 +759,19 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
     if (!c) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
-    if ((rc = compact(c))) return rc;
+    RC(compact(c));
     if (c->timing) { c->phase_ev[2] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream)); }
-    if ((rc = sort_records(c))) return rc;
+    RC(sort_records(c));
     if (c->timing) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }
-    if ((rc = format(c, FMT_MERGED, 1, 0, &c->d_out, &c->out_cap, &c->out_len))) return rc;
+    RC(format(c, c->sorted, c->nrec, c->arena, FMT_MERGED, 1, 0, merged_bound(c, c->nrec, false), &c->d_out,
+              &c->out_cap, &c->out_len));
     if (c->timing) {
         c->phase_ev[4] = take_event(c);
         HIPCHK(c, hipEventRecord(c->phase_ev[4], c->stream));
         c->phase_rec = true;
     }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     c->reduced = true;
+    c->part_R = 0;
     if (nkeys) *nkeys = c->nrec;
     if (nbytes) *nbytes = c->out_len;
     return WCG_OK;
@@ -455,48 +798,112 @@ int wcg_result_copy(wcg_ctx* c, uint8_t* host_out, uint64_t cap) {
     return WCG_OK;
 }
 
+int wcg_result_copy_device(wcg_ctx* c, void* dev_dst) {
+    if (!c) return WCG_EINVAL;
+    if (!c->reduced) { c->err = "wcg_result_copy_device before wcg_reduce"; return WCG_ESTATE; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    if (c->out_len) HIPCHK(c, hipMemcpyAsync(dev_dst, c->d_out, c->out_len, hipMemcpyDeviceToDevice, c->stream));
+    return WCG_OK;
+}
+
+int wcg_sync(wcg_ctx* c) {
+    if (!c) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return WCG_OK;
+}
+
+int wcg_partition_all(wcg_ctx* c, uint32_t nreduce, uint8_t* host_out, uint64_t cap, uint64_t* part_bytes) {
+    if (!c) return WCG_EINVAL;
+    if (!c->reduced) { c->err = "wcg_partition_all before wcg_reduce"; return WCG_ESTATE; }
+    if (nreduce == 0) { c->err = "wcg_partition_all: nreduce 0"; return WCG_EINVAL; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    RC(partition_all(c, nreduce));
+    u64 total = 0;
+    for (u32 r = 0; r < nreduce; r++) {
+        if (part_bytes) part_bytes[r] = c->part_bytes[r];
+        total += c->part_bytes[r];
+    }
+    if (host_out) {
+        if (cap < total) { c->err = "wcg_partition_all: buffer too small"; return WCG_EINVAL; }
+        if (total) {
+            HIPCHK(c, hipMemcpyAsync(host_out, c->d_part, total, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+        }
+    }
+    return WCG_OK;
+}
+
 int wcg_partition(wcg_ctx* c, uint32_t nreduce, uint32_t r, uint8_t* host_out, uint64_t cap, uint64_t* nbytes) {
     if (!c) return WCG_EINVAL;
     if (!c->reduced) { c->err = "wcg_partition before wcg_reduce"; return WCG_ESTATE; }
     if (nreduce == 0 || r >= nreduce) { c->err = "wcg_partition: bad partition"; return WCG_EINVAL; }
     int rc = set_dev(c);
     if (rc) return rc;
-    u64 len = 0;
-    if ((rc = format(c, FMT_JSON, nreduce, r, &c->d_part, &c->part_cap, &len))) return rc;
+    RC(partition_all(c, nreduce));
+    u64 off = 0;
+    for (u32 q = 0; q < r; q++) off += c->part_bytes[q];
+    const u64 len = c->part_bytes[r];
     if (nbytes) *nbytes = len;
     if (host_out) {
         if (cap < len) { c->err = "wcg_partition: buffer too small"; return WCG_EINVAL; }
-        if (len) HIPCHK(c, hipMemcpyAsync(host_out, c->d_part, len, hipMemcpyDeviceToHost, c->stream));
+        if (len) {
+            HIPCHK(c, hipMemcpyAsync(host_out, c->d_part + off, len, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+        }
     }
+    return WCG_OK;
+}
+
+int wcg_export_count(wcg_ctx* c, uint32_t nreduce, uint32_t nranks, uint64_t* counts) {
+    if (!c || !counts || nreduce == 0 || nranks == 0 || nranks > EX_MAX_RANKS) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    RC(compact(c));
+    const u64 n = c->nrec;
+    RC(ensure(c, &c->owner, &c->owner_cap, n + 1));
+    HIPCHK(c, hipMemsetAsync(c->d_per_rank, 0, EX_MAX_RANKS * sizeof(u64), c->stream));
+    if (n) {
+        k_export_count<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(c->recA, n, nreduce, nranks, c->arena,
+                                                                            c->owner, c->d_per_rank);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipMemcpyAsync(counts, c->d_per_rank, nranks * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    u64 tot = 0;
+    for (u32 i = 0; i < nranks; i++) { c->h_cur[i] = tot; tot += counts[i]; }
+    c->exp_total = tot;
+    c->exp_nranks = nranks;
+    c->exp_ready = true;
+    return WCG_OK;
+}
+
+int wcg_export_write(wcg_ctx* c, void* dev_dst) {
+    if (!c) return WCG_EINVAL;
+    if (!c->exp_ready || !c->compacted) { c->err = "wcg_export_write without wcg_export_count"; return WCG_ESTATE; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    const u64 n = c->nrec;
+    if (n && !dev_dst) return WCG_EINVAL;
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(c->d_per_rank + EX_MAX_RANKS, c->h_cur, c->exp_nranks * sizeof(u64),
+                                 hipMemcpyHostToDevice, c->stream));
+        k_export_write<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(
+            c->recA, n, c->exp_nranks, c->owner, c->d_per_rank + EX_MAX_RANKS, c->arena, (Rec*)dev_dst);
+        HIPCHK(c, hipGetLastError());
+    }
+    c->exp_ready = false;          // the cursors were consumed (the pinned copy is in flight)
     return WCG_OK;
 }
 
 int wcg_export(wcg_ctx* c, uint32_t nreduce, uint32_t nranks, const void** dev_records, uint64_t* counts) {
-    if (!c || !counts || nreduce == 0 || nranks == 0 || nranks > EX_MAX_RANKS) return WCG_EINVAL;
-    int rc = set_dev(c);
-    if (rc) return rc;
-    if ((rc = compact(c))) return rc;
-    u64 n = c->nrec;
-    HIPCHK(c, hipMemsetAsync(c->d_per_rank, 0, 2 * 1024 * sizeof(u64), c->stream));
-    if (n) {
-        k_export_count<<<(unsigned)((n + EX_TILE - 1) / EX_TILE), EX_NT, 0, c->stream>>>(c->recA, n, nreduce, nranks,
-                                                                                        c->arena, c->owner, c->d_per_rank);
-        HIPCHK(c, hipGetLastError());
-    }
-    std::vector<u64> per(nranks), cur(nranks);
-    HIPCHK(c, hipMemcpyAsync(per.data(), c->d_per_rank, nranks * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    u64 tot = 0;
-    for (u32 i = 0; i < nranks; i++) { cur[i] = tot; tot += per[i]; counts[i] = per[i]; }
-    rc = ensure(c, reinterpret_cast<uint8_t**>(&c->exp_buf), &c->exp_cap, (tot + 1) * sizeof(Rec));
-    if (rc) return rc;
-    if (n) {
-        HIPCHK(c, hipMemcpyAsync(c->d_per_rank + 1024, cur.data(), nranks * sizeof(u64), hipMemcpyHostToDevice, c->stream));
-        k_export_write<<<(unsigned)((n + EX_TILE - 1) / EX_TILE), EX_NT, 0, c->stream>>>(
-            c->recA, n, nranks, c->owner, c->d_per_rank + 1024, c->arena, c->exp_buf);
-        HIPCHK(c, hipGetLastError());
-    }
+    if (!c || !counts) return WCG_EINVAL;
+    RC(wcg_export_count(c, nreduce, nranks, counts));
+    RC(ensure(c, &c->exp_buf, &c->exp_cap, c->exp_total + 1));
+    RC(wcg_export_write(c, c->exp_buf));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (dev_records) *dev_records = c->exp_buf;
     return WCG_OK;
@@ -513,7 +920,114 @@ int wcg_import(wcg_ctx* c, const void* dev_records, uint64_t nrecords) {
                                                                           c->arena, c->arena_cap, c->st);
     HIPCHK(c, hipGetLastError());
     c->compacted = c->reduced = false;
-    return check_status(c);
+    c->exp_ready = false;
+    c->part_R = 0;
+    return WCG_OK;          // a full table is reported by the next wcg_reduce / wcg_export_count
+}
+
+int wcg_merge_runs(wcg_ctx* c, const void* dev_text, const uint64_t* run_bytes, uint32_t nruns, uint64_t* nkeys,
+                   uint64_t* nbytes) {
+    if (!c || (nruns && !run_bytes)) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    u64 total = 0;
+    for (u32 r = 0; r < nruns; r++) total += run_bytes[r];
+    c->compacted = false;
+    c->exp_ready = false;
+    c->part_R = 0;
+    c->reduced = false;
+    if (total == 0) {
+        c->nrec = 0; c->out_len = 0; c->reduced = true;
+        if (nkeys) *nkeys = 0;
+        if (nbytes) *nbytes = 0;
+        return WCG_OK;
+    }
+    if (!dev_text) return WCG_EINVAL;
+    const uint8_t* text = (const uint8_t*)dev_text;
+    const u64 nb = cdiv(total, NL_BLK);
+    RC(ensure(c, &c->lens, &c->lens_cap, nb + 1));
+    HIPCHK(c, hipMemsetAsync(&c->st->bad_input, 0, sizeof(u32), c->stream));
+    k_nl_count<<<(unsigned)nb, NL_NT, 0, c->stream>>>(text, total, c->lens);
+    k_scan_u64<<<1, 1024, 0, c->stream>>>(c->lens, nb, c->d_scalar);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const u64 L = *c->h_scalar;
+    if (L == 0) { c->err = "wcg_merge_runs: no complete line"; return WCG_EINVAL; }
+    RC(dbg(c, "merge_runs: line count"));
+    RC(ensure(c, &c->nlpos, &c->nlpos_cap, L));
+    RC(ensure_recs(c, L));
+    k_nl_recs<<<(unsigned)nb, NL_NT, 0, c->stream>>>(text, total, c->lens, c->nlpos);
+    k_line_recs<<<grid_for(L, 256, c->ncu * 8), 256, 0, c->stream>>>(text, c->nlpos, L, c->recA, c->st);
+    RC(dbg(c, "merge_runs: line records"));
+    // run boundaries in line records
+    if (c->h_rb_cap < nruns + 1) {
+        if (c->h_rb) HIPCHK(c, hipHostFree(c->h_rb));
+        HIPCHK(c, hipHostMalloc(&c->h_rb, (nruns + 1) * sizeof(u64), hipHostMallocDefault));
+        c->h_rb_cap = nruns + 1;
+    }
+    RC(ensure(c, &c->d_rb, &c->rb_cap, nruns + 1));
+    RC(ensure(c, &c->d_b0, &c->rb_cap, nruns + 1));
+    u64 acc = 0;
+    for (u32 r = 0; r <= nruns; r++) { c->h_rb[r] = acc; if (r < nruns) acc += run_bytes[r]; }
+    HIPCHK(c, hipMemcpyAsync(c->d_rb, c->h_rb, (nruns + 1) * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    k_run_bounds<<<(unsigned)cdiv(nruns + 1, 256), 256, 0, c->stream>>>(c->nlpos, L, c->d_rb, nruns, c->d_b0);
+    HIPCHK(c, hipGetLastError());
+    RC(dbg(c, "merge_runs: run bounds"));
+    Rec *src = c->recA, *dst = c->recB;
+    for (u32 s = 1; s < nruns; s *= 2) {
+        k_merge_runs<<<(unsigned)cdiv(L, MG_CHUNK), MG_NT, 0, c->stream>>>(src, dst, c->d_b0, nruns, s);
+        HIPCHK(c, hipGetLastError());
+        std::swap(src, dst);
+        RC(dbg(c, "merge_runs: merge pass"));
+    }
+    c->sorted = src;
+    c->nrec = L;
+    RC(fix_ties(c, src, L, text, dst));
+    RC(dbg(c, "merge_runs: ties"));
+    RC(format(c, src, L, text, FMT_COPY, 1, 0, total, &c->d_out, &c->out_cap, &c->out_len));
+    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_st->bad_input) { c->err = "wcg_merge_runs: a line is not \"key: count\""; return WCG_EINVAL; }
+    c->reduced = true;
+    if (nkeys) *nkeys = L;
+    if (nbytes) *nbytes = c->out_len;
+    return WCG_OK;
+}
+
+int wcg_map_json(wcg_ctx* c, const uint8_t* host_bytes, uint64_t n, uint32_t nreduce, uint8_t* host_out, uint64_t cap,
+                 uint64_t* part_bytes) {
+    if (!c || nreduce == 0 || (n && !host_bytes)) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    c->jparts.assign(nreduce, 0);
+    if (n) {
+        RC(ensure(c, &c->d_jin, &c->jin_cap, n + 64));
+        HIPCHK(c, hipMemcpyAsync(c->d_jin, host_bytes, n, hipMemcpyHostToDevice, c->stream));
+        const u64 W = cdiv(n, (u64)JS_NT * JS_SUB);
+        const u64 m = (u64)nreduce * W;
+        RC(ensure(c, &c->jhist, &c->jhist_cap, m + 1));
+        k_json_count<<<(unsigned)W, JS_NT, 0, c->stream>>>(c->d_jin, n, nreduce, c->jhist);
+        k_scan_u64<<<1, 1024, 0, c->stream>>>(c->jhist, m, c->jhist + m);
+        HIPCHK(c, hipGetLastError());
+        std::vector<u64> off(m + 1);
+        HIPCHK(c, hipMemcpyAsync(off.data(), c->jhist, (m + 1) * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        for (u32 r = 0; r < nreduce; r++) c->jparts[r] = off[(u64)(r + 1) * W] - off[(u64)r * W];
+        const u64 total = off[m];
+        if (total) {
+            RC(ensure(c, &c->d_jout, &c->jout_cap, total + 64));
+            k_json_write<<<(unsigned)W, JS_NT, 0, c->stream>>>(c->d_jin, n, nreduce, c->jhist, c->d_jout);
+            HIPCHK(c, hipGetLastError());
+        }
+        if (host_out) {
+            if (cap < total) { c->err = "wcg_map_json: buffer too small"; return WCG_EINVAL; }
+            if (total) HIPCHK(c, hipMemcpyAsync(host_out, c->d_jout, total, hipMemcpyDeviceToHost, c->stream));
+        }
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (part_bytes) for (u32 r = 0; r < nreduce; r++) part_bytes[r] = c->jparts[r];
+    return WCG_OK;
 }
 
 int wcg_timings(wcg_ctx* c, double* ms, int n, uint64_t* map_launches) {

@@ -81,6 +81,8 @@ struct DevState {
     u64 nlong;           // ... of which long keys (> 15 bytes)
     u32 overflow;        // table / arena full -> WCG_EFULL
     u32 spin_fail;       // bounded spin gave up -> WCG_EFULL (never expected)
+    u32 bad_input;       // malformed record units (wcg_import) or lines (wcg_merge_runs) -> WCG_EINVAL
+    u32 pad_;
 };
 
 // ------------------------------------------------------------------ letters

@@ -1,0 +1,106 @@
+// wcg_ingest.h - host side of the GPU Split (mapreduce.go:141-179): input bytes reach HBM in
+// line-aligned chunks through two pinned staging buffers, so the PCIe copy of chunk k + 1 and the
+// host read of chunk k + 2 overlap the map kernels of chunk k.
+//
+//   reader threads (a small pool) fill pinned buffer k % 2 from the source (pread of a file, or
+//   memcpy of a pageable host split) and scan their slice for '\n' as they go;
+//   the chunk is cut after its last '\n' (a partial line moves to the front of the next buffer),
+//   so no line, token or rune straddles a chunk;
+//   Split's 64 KiB line limit (quirk P1) is emulated: the first line that does not fit
+//   bufio.Scanner's buffer with its '\n' ends the input, as it ends the reference's scan;
+//   the copy stream waits until device buffer k % 2 is free (its previous map kernels are done),
+//   copies, and the map stream waits for the copy.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace wcg {
+
+// fixed pool of worker threads running one batch of indexed tasks at a time
+class TaskPool {
+  public:
+    explicit TaskPool(int n) {
+        for (int i = 0; i < n; i++) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~TaskPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    // run f(0..n-1) on the pool and wait for all of them
+    void run(int n, const std::function<void(int)>& f) {
+        std::unique_lock<std::mutex> g(m_);
+        f_ = &f;
+        ntask_ = n;
+        next_ = 0;
+        done_ = 0;
+        gen_++;
+        cv_.notify_all();
+        done_cv_.wait(g, [&] { return done_ == ntask_; });
+        f_ = nullptr;
+    }
+
+  private:
+    void loop(int) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> g(m_);
+        while (true) {
+            cv_.wait(g, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (stop_) return;
+            while (f_ && next_ < ntask_) {
+                const int t = next_++;
+                const std::function<void(int)>* f = f_;
+                g.unlock();
+                (*f)(t);
+                g.lock();
+                if (++done_ == ntask_) done_cv_.notify_all();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)>* f_ = nullptr;
+    int ntask_ = 0, next_ = 0, done_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+constexpr uint64_t SCAN_MAX_LINE = 65536;   // bufio.MaxScanTokenSize: a line + '\n' must fit
+
+// '\n' structure of one reader slice [a, b) of a chunk
+struct SliceLines {
+    int64_t first = -1, last = -1;   // first / last '\n' in the slice (-1: none)
+    int64_t bad = -1;                // start of the first over-long line wholly inside the slice
+};
+
+inline SliceLines scan_slice(const uint8_t* p, int64_t a, int64_t b) {
+    SliceLines s;
+    int64_t prev = -1;
+    for (int64_t i = a; i < b;) {
+        const void* q = memchr(p + i, '\n', (size_t)(b - i));
+        if (!q) break;
+        const int64_t nl = (const uint8_t*)q - p;
+        if (s.first < 0) s.first = nl;
+        else if (s.bad < 0 && nl - (prev + 1) >= (int64_t)SCAN_MAX_LINE) s.bad = prev + 1;
+        prev = nl;
+        i = nl + 1;
+    }
+    s.last = prev;
+    return s;
+}
+
+}  // namespace wcg

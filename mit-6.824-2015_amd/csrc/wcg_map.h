@@ -72,6 +72,7 @@ struct MapArgs {
     u32* llog_len;                 // records written per region
 };
 constexpr u64 LLOG_OFF_MASK = (1ull << 40) - 1;   // record = input offset | len << 40 (len 0: walk)
+constexpr u32 LLOG_PER_STEP = 16;                 // long-token log records per step (average)
 
 // append one miss-log entry (wcg_lds_table.h) for this workgroup; false when the region is
 // full (the units of a region's last, cut-off entry are zeroed so k_agg skips them)
@@ -205,10 +206,6 @@ __device__ void long_token(const MapArgs& a, u64 p) {
     });
 }
 
-// long token (> 15 bytes) starting at window offset rp (absolute offset p): its length from
-// the wave's chunk letter masks and its bytes from the staged window, both in LDS - a per-rune
-// walk through global memory is a chain of dependent loads per byte.  A run that reaches the
-// look-ahead chunk may continue past the window: that one takes the global walk.
 // long token (> 15 bytes) starting at window offset rp (absolute offset p): its length from the
 // wave's chunk letter masks (LDS), then one record in the workgroup's long-token log; k_long
 // counts it.  A run that reaches the look-ahead chunk may continue past the window: its record
@@ -230,7 +227,7 @@ __device__ __forceinline__ void long_token_log(const MapArgs& a, u64 p, u32 rp, 
     if (ABL == 7) { asm volatile("" ::"v"(len)); return; }
     const u32 pos = atomicAdd(lcur, 1u);
     if (pos < a.llog_cap) a.llog[(u64)blockIdx.x * a.llog_cap + pos] = p | (u64)len << 40;
-    else atomicAdd(&a.st->overflow, 1u);           // cannot happen: 60 records per step bound it
+    else long_token(a, p);              // region full (dense long tokens): count it here, exactly
 }
 
 // k_long: count the logged long tokens in the long-key table.  Workgroup b serves map region
@@ -241,9 +238,12 @@ __device__ __forceinline__ void long_token_log(const MapArgs& a, u64 p, u32 rp, 
 // occurs 1.2e5 times per GiB; the count atomics were 5 of k_long's 12 ms).  A workgroup caches
 // {tag, len, slot, arena offset} of the keys it has counted in LDS; an occurrence whose tag and
 // length match a cached key compares its bytes with the key's arena cell (exact, 16-byte loads)
-// and counts in LDS; the LDS counts are added to the table once at the end.  Cache entries are
-// filled in one round and read only in later rounds (after the round's barrier), so no lane
-// waits on another's LDS write.
+// and counts in LDS; the LDS counts are added to the table once at the end.  A lane never waits
+// on another's LDS write: an entry being filled in the same round may be seen half-written (tag
+// set, offset still 0 or length stale), and such a probe simply falls through to ltab_add.
+// Correctness rests on the exact match (tag, length, then the key's bytes against its real arena
+// cell, with coff == 0 treated as "not filled"), not on when entries become visible; cslot is
+// read only after the final barrier.
 constexpr int LONG_NT = 256;
 constexpr int LONG_PARTS = 8;
 constexpr int LCACHE = 1024;                  // LDS cache entries (28 B each)
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(LONG_NT) void k_long(MapArgs a, u32 nreg, int mode)
     const u32 stride = LONG_PARTS * LONG_NT, first = part * LONG_NT;
     const u32 rounds = nrec > first ? (nrec - first + stride - 1) / stride : 0;   // workgroup-uniform
     if (rounds == 0) return;          // ASCII text: nearly every workgroup (no barrier reached yet)
-    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; coff[e] = 0; ccnt[e] = 0; }
+    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; coff[e] = 0; ccnt[e] = 0; clen[e] = 0; }
     __syncthreads();
     const uint8_t* in = a.in;
     const u64 n = a.n;

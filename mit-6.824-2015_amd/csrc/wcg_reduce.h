@@ -1,14 +1,19 @@
 // wcg_reduce.h - DoReduce + Merge on gfx950 (mapreduce.go:239-321, wc.go:35-38).
 //
 //   k_compact   global tables -> dense records {128-bit big-endian prefix, count, ref}
-//   k_tile_sort / k_merge   merge sort by the 128-bit big-endian prefix (fact F4 makes the
-//               zero-padded prefix Go's sort.Strings order for keys <= 15 bytes)
-//   k_tie_fix   long keys (> 15 bytes) that share a 16-byte prefix: ordered by full bytes
-//   k_fmt_sum / k_scan_u64 / k_fmt_write  "key: count\n" (Merge, mapreduce.go:316-318) or
-//               {"Key":"k","Value":"count"}\n for ihash(k)%R == r (DoReduce, :274-278)
+//   (the sort: wcg_sort.h)
+//   k_fmt_sum / k_scan_u64 / k_fmt_write  "key: count\n" (Merge, mapreduce.go:316-318),
+//               {"Key":"k","Value":"count"}\n lines (DoReduce, :274-278), or line copies (the
+//               merge of formatted runs)
+//   k_part_hist / k_part_scatter  records grouped by ihash(key) % R, each group in key order:
+//               every -res-<r> file in one formatting pass
+//   k_json_count / k_json_write  DoMap's per-occurrence JSON lines (mapreduce.go:214-230)
+//   k_nl_*      line index of formatted runs (the cross-GPU Merge input)
+//   k_export_* / k_import  the ihash % nReduce shuffle between GPUs
 #pragma once
 #include "wcg_common.h"
 #include "wcg_lds_table.h"
+#include "wcg_sort.h"
 
 namespace wcg {
 
@@ -45,7 +50,7 @@ __device__ __forceinline__ bool slot_to_rec(const GEntry* gtab, u64 gslots, cons
 }
 
 __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
-                                                  const uint8_t* arena, Rec* out, DevState* st) {
+                                                  const uint8_t* arena, Rec* out, u64 cap, DevState* st) {
     __shared__ u32 wsum[CP_NT / 64];
     __shared__ u64 base_s;
     const u64 total = gslots + lslots;
@@ -80,189 +85,7 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
     u64 pos = base_s + wsum[w] + o;
 #pragma unroll
     for (int j = 0; j < CP_IPT; j++)
-        if (have & (1u << j)) out[pos++] = r[j];
-}
-
-// ---------------------------------------------------------------- sort
-// Merge sort on the 128-bit big-endian prefix: k_tile_sort orders each 2048-record tile with an
-// LDS bitonic network, then log2(n / 2048) k_merge passes double the sorted run length.  Cost
-// does not depend on the key distribution (a radix sort's MSD buckets collapse on UTF-8 text,
-// where every word of a script shares its first byte or two) and no pass needs the host.
-constexpr int TS_NT = 1024, TS_TILE = 2048;
-constexpr int MG_NT = 256, MG_CHUNK = 1024;
-
-__device__ __forceinline__ bool pre_lt(u64 ah, u64 al, u64 bh, u64 bl) { return ah < bh || (ah == bh && al < bl); }
-
-__global__ __launch_bounds__(TS_NT) void k_tile_sort(const Rec* in, Rec* out, u64 n) {
-    __shared__ u64 sh[TS_TILE], sl[TS_TILE];
-    __shared__ uint16_t si[TS_TILE];
-    const u64 base = (u64)blockIdx.x * TS_TILE;
-    const int tid = threadIdx.x;
-    for (int k = 0; k < TS_TILE / TS_NT; k++) {
-        const int i = k * TS_NT + tid;
-        const u64 g = base + i;
-        if (g < n) {
-            const Rec r = in[g];
-            sh[i] = r.hi; sl[i] = r.lo;
-        } else {                                  // padding: no key has an all-0xFF prefix
-            sh[i] = ~0ull; sl[i] = ~0ull;
-        }
-        si[i] = (uint16_t)i;
-    }
-    __syncthreads();
-    for (int k = 2; k <= TS_TILE; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-            for (int q = 0; q < TS_TILE / 2 / TS_NT; q++) {
-                const int t = q * TS_NT + tid;               // compare-exchange pair t
-                const int i = 2 * t - (t & (j - 1)), p = i + j;
-                const u64 ah = sh[i], al = sl[i], bh = sh[p], bl = sl[p];
-                if (pre_lt(bh, bl, ah, al) == ((i & k) == 0)) {
-                    sh[i] = bh; sl[i] = bl; sh[p] = ah; sl[p] = al;
-                    const uint16_t x = si[i]; si[i] = si[p]; si[p] = x;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int k = 0; k < TS_TILE / TS_NT; k++) {
-        const int i = k * TS_NT + tid;
-        if (base + i < n) out[base + i] = in[base + si[i]];
-    }
-}
-
-// merge path: number of A records among the first d outputs of merge(A, B) (A first on equal
-// prefixes).  One wave, 64-way search: each round samples 64 split candidates, so a run of a
-// million records is settled in four rounds of two loads each.
-__device__ __forceinline__ u64 merge_split(const Rec* A, u64 la, const Rec* B, u64 lb, u64 d, int lane) {
-    u64 lo = d > lb ? d - lb : 0, hi = d < la ? d : la;
-    while (hi > lo) {
-        const u64 s = hi - lo;
-        const u64 p = s <= 64 ? lo + lane : lo + (u64)lane * s / 64;
-        bool t = false;
-        if (p < hi) {
-            const Rec& x = A[p];
-            const Rec& y = B[d - 1 - p];
-            t = !pre_lt(y.hi, y.lo, x.hi, x.lo);
-        }
-        const int c = __popcll(__ballot(t));
-        if (s <= 64) return lo + c;
-        const u64 nlo = c > 0 ? __shfl(p, c - 1) + 1 : lo;
-        const u64 nhi = c < 64 ? __shfl(p, c) : hi;
-        lo = nlo; hi = nhi;
-    }
-    return lo;
-}
-
-// one merge pass: runs of length w -> 2w; workgroup b writes outputs [b * 1024, +1024)
-__global__ __launch_bounds__(MG_NT) void k_merge(const Rec* in, Rec* out, u64 n, u64 w) {
-    __shared__ u64 sh[MG_CHUNK], sl[MG_CHUNK];
-    __shared__ u64 split[2];
-    const u64 c0 = (u64)blockIdx.x * MG_CHUNK;
-    const u64 a0 = c0 / (2 * w) * (2 * w);
-    const u64 la = n - a0 < w ? n - a0 : w;
-    const u64 rest = n - a0 - la;
-    const u64 lb = rest < w ? rest : w;
-    const Rec* A = in + a0;
-    const Rec* B = A + la;
-    const u64 d0 = c0 - a0, d1 = (d0 + MG_CHUNK < la + lb) ? d0 + MG_CHUNK : la + lb;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (wv < 2) {
-        const u64 sp = merge_split(A, la, B, lb, wv ? d1 : d0, lane);
-        if (lane == 0) split[wv] = sp;
-    }
-    __syncthreads();
-    const u64 i0 = split[0], i1 = split[1];
-    const u64 j0 = d0 - i0;
-    const int na = (int)(i1 - i0), m = (int)(d1 - d0);
-    Rec r[MG_CHUNK / MG_NT];
-#pragma unroll
-    for (int k = 0; k < MG_CHUNK / MG_NT; k++) {
-        const int e = k * MG_NT + tid;
-        if (e < m) {
-            r[k] = e < na ? A[i0 + e] : B[j0 + (e - na)];
-            sh[e] = r[k].hi; sl[e] = r[k].lo;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < MG_CHUNK / MG_NT; k++) {
-        const int e = k * MG_NT + tid;
-        if (e >= m) continue;
-        const u64 xh = r[k].hi, xl = r[k].lo;
-        int lo, hi, pos;
-        if (e < na) {                              // B window records strictly below x
-            lo = na; hi = m;
-            while (lo < hi) { const int mid = (lo + hi) >> 1; if (pre_lt(sh[mid], sl[mid], xh, xl)) lo = mid + 1; else hi = mid; }
-            pos = e + (lo - na);
-        } else {                                   // A window records at or below x
-            lo = 0; hi = na;
-            while (lo < hi) { const int mid = (lo + hi) >> 1; if (!pre_lt(xh, xl, sh[mid], sl[mid])) lo = mid + 1; else hi = mid; }
-            pos = (e - na) + lo;
-        }
-        out[a0 + d0 + pos] = r[k];
-    }
-}
-
-// exclusive scan of u64 (in place) by one workgroup of 1024 threads; total in *total
-__global__ __launch_bounds__(1024) void k_scan_u64(u64* v, u64 n, u64* total) {
-    __shared__ u64 ws[16];
-    __shared__ u64 carry_s;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) carry_s = 0;
-    __syncthreads();
-    for (u64 base = 0; base < n; base += 1024 * 4) {
-        u64 x[4], s = 0;
-        for (int k = 0; k < 4; k++) {
-            u64 i = base + (u64)tid * 4 + k;
-            x[k] = i < n ? v[i] : 0;
-            s += x[k];
-        }
-        u64 incl = s;
-        for (int d = 1; d < 64; d <<= 1) { u64 y = __shfl_up(incl, d, 64); if (lane >= d) incl += y; }
-        if (lane == 63) ws[w] = incl;
-        __syncthreads();
-        u64 wpre = 0, all = 0;
-        for (int k = 0; k < 16; k++) { if (k < w) wpre += ws[k]; all += ws[k]; }
-        u64 run = carry_s + wpre + incl - s;
-        for (int k = 0; k < 4; k++) {
-            u64 i = base + (u64)tid * 4 + k;
-            if (i < n) v[i] = run;
-            run += x[k];
-        }
-        __syncthreads();
-        if (tid == 0) carry_s += all;
-        __syncthreads();
-    }
-    if (tid == 0 && total) *total = carry_s;
-}
-
-// ---------------------------------------------------------------- long-key ties
-__device__ int cmp_full(const Rec& a, const Rec& b, const uint8_t* arena) {
-    // both long: compare full bytes
-    u64 la = (a.ref >> 40) & LONG_LEN_MAX, lb = (b.ref >> 40) & LONG_LEN_MAX;
-    const uint8_t* pa = arena + (a.ref & LONG_OFF_MASK);
-    const uint8_t* pb = arena + (b.ref & LONG_OFF_MASK);
-    u64 m = la < lb ? la : lb;
-    for (u64 i = 0; i < m; i++) if (pa[i] != pb[i]) return pa[i] < pb[i] ? -1 : 1;
-    return la < lb ? -1 : (la > lb ? 1 : 0);
-}
-
-// one thread per run of equal prefixes: insertion sort by full key bytes
-__global__ void k_tie_fix(Rec* r, u64 n, const uint8_t* arena) {
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i + 1 < n; i += (u64)gridDim.x * blockDim.x) {
-        bool start = (r[i].hi == r[i + 1].hi && r[i].lo == r[i + 1].lo) &&
-                     (i == 0 || r[i - 1].hi != r[i].hi || r[i - 1].lo != r[i].lo);
-        if (!start) continue;
-        u64 e = i + 1;
-        while (e + 1 < n && r[e + 1].hi == r[i].hi && r[e + 1].lo == r[i].lo) e++;
-        for (u64 a = i + 1; a <= e; a++) {
-            Rec x = r[a];
-            u64 b = a;
-            while (b > i && cmp_full(r[b - 1], x, arena) > 0) { r[b] = r[b - 1]; b--; }
-            r[b] = x;
-        }
-    }
+        if (have & (1u << j)) { if (pos < cap) out[pos] = r[j]; pos++; }   // more: host grows, reruns
 }
 
 // ---------------------------------------------------------------- formatting
@@ -278,16 +101,27 @@ __device__ __forceinline__ u32 rec_byte(const Rec& r, u64 k, const uint8_t* aren
 }
 __device__ u32 rec_ihash(const Rec& r, const uint8_t* arena) {
     u32 h = 0x811C9DC5u;
-    u64 len = rec_len(r);
-    for (u64 k = 0; k < len; k++) h = fnv1a_step(h, rec_byte(r, k, arena));
+    const u64 len = rec_len(r);
+    if (!(r.ref & LONG_FLAG)) {            // inline key: its bytes are the prefix words
+        for (u64 k = 0; k < len; k++) h = fnv1a_step(h, k < 8 ? (u32)(r.hi >> (56 - 8 * k)) & 0xFF
+                                                              : (u32)(r.lo >> (120 - 8 * k)) & 0xFF);
+        return h;
+    }
+    const uint8_t* p = arena + (r.ref & LONG_OFF_MASK);
+    for (u64 k = 0; k < len; k++) h = fnv1a_step(h, p[k]);
     return h;
 }
 
-constexpr int FMT_MERGED = 0, FMT_JSON = 1;
+// FMT_MERGED "key: count\n"; FMT_JSON {"Key":"k","Value":"count"}\n for ihash(k) % nreduce ==
+// part; FMT_JSON_ALL the same for every record (records pre-grouped by partition); FMT_COPY
+// copies line records of formatted text (cnt = line bytes, ref & LONG_OFF_MASK = offset in `arena`)
+constexpr int FMT_MERGED = 0, FMT_JSON = 1, FMT_JSON_ALL = 2, FMT_COPY = 3;
 constexpr u64 JSON_FIXED = 8 + 11 + 3;   // {"Key":" + ","Value":" + "}\n
 
 __device__ __forceinline__ u64 line_len(const Rec& x, int fmt, u32 nreduce, u32 part, const uint8_t* arena) {
     if (fmt == FMT_MERGED) return rec_len(x) + 3 + ndigits(x.cnt);
+    if (fmt == FMT_COPY) return x.cnt;
+    if (fmt == FMT_JSON_ALL) return rec_len(x) + JSON_FIXED + ndigits(x.cnt);
     return (rec_ihash(x, arena) % nreduce == part) ? rec_len(x) + JSON_FIXED + ndigits(x.cnt) : 0;
 }
 
@@ -334,13 +168,20 @@ __global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, int fm
     for (int q = 0; q < FM_IPT; q++) {
         if (L[q] == 0) continue;
         const Rec x = r[i0 + q];
+        if (fmt == FMT_COPY) {
+            const uint8_t* src = arena + (x.ref & LONG_OFF_MASK);
+            for (u64 k = 0; k < L[q]; k++) o[k] = src[k];
+            o += L[q];
+            continue;
+        }
+        const bool json = fmt != FMT_MERGED;
         const u64 len = rec_len(x);
-        if (fmt == FMT_JSON) {
+        if (json) {
             const char* pre = "{\"Key\":\"";
             for (int k = 0; k < 8; k++) *o++ = pre[k];
         }
         for (u64 k = 0; k < len; k++) *o++ = (uint8_t)rec_byte(x, k, arena);
-        if (fmt == FMT_JSON) {
+        if (json) {
             const char* mid = "\",\"Value\":\"";
             for (int k = 0; k < 11; k++) *o++ = mid[k];
         } else {
@@ -350,9 +191,223 @@ __global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, int fm
         u64 c = x.cnt;
         for (int k = (int)nd - 1; k >= 0; k--) { o[k] = (uint8_t)('0' + c % 10); c /= 10; }
         o += nd;
-        if (fmt == FMT_JSON) { *o++ = '"'; *o++ = '}'; }
+        if (json) { *o++ = '"'; *o++ = '}'; }
         *o++ = '\n';
     }
+}
+
+// ---------------------------------------------------------------- every -res-<r> at once
+// The sorted records are regrouped by partition p = ihash(key) % R, stably (each group keeps
+// key order), so one formatting pass writes all R DoReduce files back to back.  Tiles of
+// PT_TILE records: k_part_hist counts records (and JSON bytes) per (p, tile); after a scan,
+// k_part_scatter places each record at its group offset + its rank among the tile's earlier
+// records of the same partition (wave ballots on the partition bits give the rank in order).
+constexpr int PT_NT = 256, PT_TILE = 1024;
+constexpr u32 PT_MAXR = 1024;
+
+__global__ __launch_bounds__(PT_NT) void k_part_hist(const Rec* r, u64 n, u32 R, const uint8_t* arena, u32* pid,
+                                                     u32* hist, u64* part_bytes) {
+    __shared__ u32 c[PT_MAXR];
+    __shared__ u64 bsum[PT_MAXR];
+    for (u32 p = threadIdx.x; p < R; p += PT_NT) { c[p] = 0; bsum[p] = 0; }
+    __syncthreads();
+    const u64 T = (n + PT_TILE - 1) / PT_TILE;
+    for (int k = 0; k < PT_TILE / PT_NT; k++) {
+        const u64 i = (u64)blockIdx.x * PT_TILE + k * PT_NT + threadIdx.x;
+        if (i >= n) continue;
+        const Rec x = r[i];
+        const u32 p = rec_ihash(x, arena) % R;
+        pid[i] = p;
+        atomicAdd(&c[p], 1u);
+        atomicAdd((unsigned long long*)&bsum[p], (unsigned long long)(rec_len(x) + JSON_FIXED + ndigits(x.cnt)));
+    }
+    __syncthreads();
+    for (u32 p = threadIdx.x; p < R; p += PT_NT) {
+        hist[(u64)p * T + blockIdx.x] = c[p];
+        if (bsum[p]) atomicAdd((unsigned long long*)&part_bytes[p], (unsigned long long)bsum[p]);
+    }
+}
+
+__global__ __launch_bounds__(PT_NT) void k_part_scatter(const Rec* r, u64 n, u32 R, const u32* pid, const u32* off,
+                                                        Rec* out) {
+    __shared__ u32 base[PT_MAXR];
+    __shared__ u32 wc[PT_NT / 64][PT_MAXR];
+    const u64 T = (n + PT_TILE - 1) / PT_TILE;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (u32 p = tid; p < R; p += PT_NT) base[p] = off[(u64)p * T + blockIdx.x];
+    for (u32 q = tid; q < (PT_NT / 64) * R; q += PT_NT) wc[q / R][q % R] = 0;
+    u32 bits = 0;
+    while ((1u << bits) < R) bits++;
+    for (int k = 0; k < PT_TILE / PT_NT; k++) {
+        const u64 i = (u64)blockIdx.x * PT_TILE + k * PT_NT + tid;
+        const bool valid = i < n;
+        const u32 p = valid ? pid[i] : 0u;
+        u64 m = __ballot(valid);
+        for (u32 b = 0; b < bits; b++) {
+            const u64 bal = __ballot((p >> b) & 1);
+            m &= ((p >> b) & 1) ? bal : ~bal;
+        }
+        const u64 below = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const u32 rank = (u32)__popcll(m & below);
+        __syncthreads();                                     // base[] / wc[] of the last round used
+        if (valid && rank == 0) wc[w][p] = (u32)__popcll(m);  // the lowest lane of each partition
+        __syncthreads();
+        if (valid) {
+            u32 d = base[p] + rank;
+            for (int v = 0; v < w; v++) d += wc[v][p];        // earlier waves of this round
+            out[d] = r[i];
+        }
+        __syncthreads();
+        // advance the bases past this round's records; clear the wave counts this round set
+        if (valid && rank == 0) atomicAdd(&base[p], wc[w][p]);
+        __syncthreads();
+        if (valid && rank == 0) wc[w][p] = 0;
+    }
+}
+
+// ---------------------------------------------------------------- DoMap's JSON (-m-r) lines
+// Reference-exact map output (mapreduce.go:214-230): for every token, in input order, the line
+// {"Key":"tok","Value":"1"}\n in file ihash(tok) % R.  Each thread walks its JS_SUB input bytes
+// (tokens owned by their first byte, fact F3) with the byte-exact letter test; partitions are
+// processed JS_PG at a time.  k_json_count sums line bytes per (partition, workgroup);
+// k_json_write re-walks, turns per-thread sums into in-order offsets and writes the lines.
+constexpr int JS_NT = 128;
+constexpr u64 JS_SUB = 2048;
+constexpr u32 JS_PG = 128;
+constexpr u64 JS_LINE = 23;              // {"Key":" + ","Value":"1"}\n
+
+template <typename F>
+__device__ __forceinline__ void for_tokens(const uint8_t* in, u64 n, u64 c0, u64 c1, F f) {
+    auto at = [&](long i) -> u32 { return (i >= 0 && (u64)i < n) ? in[i] : 0u; };
+    u64 p = c0;
+    if (p > 0 && p < n && letter_byte(at, (long)p - 1) && letter_byte(at, (long)p))
+        while (p < n && letter_byte(at, (long)p)) p++;              // the previous owner's token
+    while (p < c1 && p < n) {
+        if (!letter_byte(at, (long)p)) { p++; continue; }
+        u64 q = p + 1;
+        while (q < n && letter_byte(at, (long)q)) q++;
+        f(p, q - p);
+        p = q;
+    }
+}
+
+__device__ __forceinline__ u32 fnv32_bytes(const uint8_t* p, u64 len) {
+    u32 h = 0x811C9DC5u;
+    for (u64 k = 0; k < len; k++) h = fnv1a_step(h, p[k]);
+    return h;
+}
+
+__global__ __launch_bounds__(JS_NT) void k_json_count(const uint8_t* in, u64 n, u32 R, u64* hist) {
+    __shared__ unsigned long long s[JS_PG];
+    const u64 W = gridDim.x;
+    const u64 c0 = ((u64)blockIdx.x * JS_NT + threadIdx.x) * JS_SUB;
+    for (u32 pg = 0; pg < R; pg += JS_PG) {
+        for (u32 p = threadIdx.x; p < JS_PG; p += JS_NT) s[p] = 0;
+        __syncthreads();
+        for_tokens(in, n, c0, c0 + JS_SUB, [&](u64 p, u64 len) {
+            const u32 r = fnv32_bytes(in + p, len) % R;
+            if (r >= pg && r < pg + JS_PG) atomicAdd(&s[r - pg], (unsigned long long)(JS_LINE + len));
+        });
+        __syncthreads();
+        for (u32 p = threadIdx.x; p < JS_PG && pg + p < R; p += JS_NT) hist[(u64)(pg + p) * W + blockIdx.x] = s[p];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(JS_NT) void k_json_write(const uint8_t* in, u64 n, u32 R, const u64* off, uint8_t* out) {
+    __shared__ u32 t[JS_PG][JS_NT + 1];            // per-thread line bytes per partition -> offsets
+    const u64 W = gridDim.x;
+    const int tid = threadIdx.x;
+    const u64 c0 = ((u64)blockIdx.x * JS_NT + tid) * JS_SUB;
+    for (u32 pg = 0; pg < R; pg += JS_PG) {
+        for (u32 p = 0; p < JS_PG; p++) t[p][tid] = 0;
+        for_tokens(in, n, c0, c0 + JS_SUB, [&](u64 p, u64 len) {
+            const u32 r = fnv32_bytes(in + p, len) % R;
+            if (r >= pg && r < pg + JS_PG) t[r - pg][tid] += (u32)(JS_LINE + len);
+        });
+        __syncthreads();
+        for (u32 p = tid; p < JS_PG; p += JS_NT) {   // exclusive scan over the threads, in order
+            u32 run = 0;
+            for (int q = 0; q < JS_NT; q++) { const u32 v = t[p][q]; t[p][q] = run; run += v; }
+        }
+        __syncthreads();
+        for_tokens(in, n, c0, c0 + JS_SUB, [&](u64 p, u64 len) {
+            const u32 r = fnv32_bytes(in + p, len) % R;
+            if (r < pg || r >= pg + JS_PG) return;
+            uint8_t* o = out + off[(u64)r * W + blockIdx.x] + t[r - pg][tid];
+            t[r - pg][tid] += (u32)(JS_LINE + len);
+            const char* pre = "{\"Key\":\"";
+            for (int k = 0; k < 8; k++) *o++ = pre[k];
+            for (u64 k = 0; k < len; k++) *o++ = in[p + k];
+            const char* suf = "\",\"Value\":\"1\"}\n";
+            for (int k = 0; k < 15; k++) *o++ = suf[k];
+        });
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- line index (merge of runs)
+// Formatted runs "key: count\n" -> one record per line: {hi, lo} = the key's first 16 bytes
+// (big-endian, zero-padded: the sort prefix), cnt = line bytes, ref = line offset | key length
+// << 40 (| LONG_FLAG for keys of 16+ bytes: the tie groups).  k_nl_count counts '\n' per 64 KiB
+// block, k_scan_u64 makes offsets, k_nl_recs emits the records in order.
+constexpr int NL_NT = 256;
+constexpr u64 NL_BLK = 65536;
+
+__global__ __launch_bounds__(NL_NT) void k_nl_count(const uint8_t* t, u64 n, u64* cnt) {
+    __shared__ u64 ws[NL_NT / 64];
+    const u64 b0 = (u64)blockIdx.x * NL_BLK;
+    u64 c = 0;
+    for (u64 i = b0 + threadIdx.x; i < b0 + NL_BLK && i < n; i += NL_NT) c += t[i] == '\n';
+    const u64 all = block_sum_u64(c, ws);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = all;
+}
+
+__global__ __launch_bounds__(NL_NT) void k_nl_recs(const uint8_t* t, u64 n, const u64* off, u64* nlpos) {
+    // positions of the '\n' bytes, in order (one pass per block, ordered by a wave scan)
+    __shared__ u64 ws[NL_NT / 64];
+    const u64 b0 = (u64)blockIdx.x * NL_BLK;
+    u64 base = off[blockIdx.x];
+    for (u64 i0 = b0; i0 < b0 + NL_BLK && i0 < n; i0 += NL_NT) {
+        const u64 i = i0 + threadIdx.x;
+        const u64 f = (i < n && i < b0 + NL_BLK && t[i] == '\n') ? 1 : 0;
+        u64 all;
+        const u64 pre = block_excl_scan(f, ws, all);
+        if (f) nlpos[base + pre] = i;
+        base += all;
+        __syncthreads();
+    }
+}
+
+__global__ void k_line_recs(const uint8_t* t, const u64* nlpos, u64 nl, Rec* out, DevState* st) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < nl; i += (u64)gridDim.x * blockDim.x) {
+        const u64 s = i ? nlpos[i - 1] + 1 : 0, e = nlpos[i] + 1;
+        u64 k = s;
+        u64 hi = 0, lo = 0;
+        while (k < e && t[k] != ':') {                   // keys are letters: the first ':' ends it
+            const u64 j = k - s;
+            if (j < 8) hi |= (u64)t[k] << (56 - 8 * j);
+            else if (j < 16) lo |= (u64)t[k] << (120 - 8 * j);
+            k++;
+        }
+        const u64 klen = k - s;
+        if (k == e || klen == 0 || klen > LONG_LEN_MAX) atomicAdd(&st->bad_input, 1u);   // not "key: count"
+        Rec r;
+        r.hi = hi; r.lo = lo; r.cnt = e - s;
+        r.ref = (klen >= 16 ? LONG_FLAG : 0ull) | ((klen < LONG_LEN_MAX ? klen : LONG_LEN_MAX) << 40) | s;
+        out[i] = r;
+    }
+}
+
+// run r of the concatenated text starts at byte rb[r]: its first line record is the number of
+// '\n' before that byte
+__global__ void k_run_bounds(const u64* nlpos, u64 nl, const u64* rb, u32 nruns, u64* b) {
+    const u32 r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r > nruns) return;
+    const u64 x = rb[r];
+    u64 lo = 0, hi = nl;
+    while (lo < hi) { const u64 mid = (lo + hi) >> 1; if (nlpos[mid] < x) lo = mid + 1; else hi = mid; }
+    b[r] = lo;
 }
 
 // ---------------------------------------------------------------- multi-GPU shuffle
@@ -453,6 +508,10 @@ __global__ void k_import(const Rec* in, u64 n, GEntry* gtab, u64 gmask, GEntry* 
     for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
         Rec x = in[i];
         if (x.ref == CONT_MARK) continue;
+        if (!(x.ref & LONG_FLAG) ? (x.ref == 0 || x.ref > 15) : (((x.ref >> 40) & LONG_LEN_MAX) < 16)) {
+            atomicAdd(&st->bad_input, 1u);                // not a unit k_export_write produces
+            continue;
+        }
         if (!(x.ref & LONG_FLAG)) {
             u64 k0, k1;
             make_key(bswap64(x.hi), bswap64(x.lo), (int)x.ref, k0, k1);

@@ -1,0 +1,612 @@
+// wcg_sort.h - the key sort of DoReduce + Merge on gfx950 (sort.Strings, mapreduce.go:268,309).
+//
+// Records (wcg_common.h Rec) are ordered by their 128-bit big-endian key prefix, which is Go's
+// bytewise string order for keys <= 15 bytes (fact F4).  Keys of 16+ bytes that share a prefix
+// are ordered by their full bytes afterwards (tie groups).
+//
+//   sample sort   k_ss_sample -> (k_tile_sort + k_merge over the sample) -> k_ss_hist ->
+//                 scan -> k_ss_scatter -> k_ss_bucket: the sample's order statistics split the
+//                 records into B buckets of ~SS_TARGET records (sampling keeps buckets even
+//                 whatever the key distribution: UTF-8 words share their first bytes, which is
+//                 what makes an MSD radix sort's buckets collapse); every bucket is then sorted
+//                 in one workgroup's LDS.  The order is (prefix, record index), a total order, so
+//                 splitters are unique and equal prefixes cannot pile into one bucket.  Two
+//                 passes over the records instead of log2(n / 2048) merge passes.
+//   tie groups    k_tie_mark + k_tie_sort: runs of long keys with one 16-byte prefix, sorted
+//                 in parallel per group by the next 16 bytes (cached), then by the rest.
+//   merge runs    k_merge_runs: pairwise merge passes over k sorted runs (the cross-GPU Merge).
+#pragma once
+#include "wcg_common.h"
+
+namespace wcg {
+
+__device__ __forceinline__ bool pre_lt(u64 ah, u64 al, u64 bh, u64 bl) { return ah < bh || (ah == bh && al < bl); }
+__device__ __forceinline__ bool key3_lt(u64 ah, u64 al, u32 ai, u64 bh, u64 bl, u32 bi) {
+    return ah < bh || (ah == bh && (al < bl || (al == bl && ai < bi)));
+}
+
+// ---------------------------------------------------------------- merge sort (the sample, runs)
+// k_tile_sort orders each 2048-record tile by an LDS bitonic network, stable (ties by position),
+// then k_merge passes double the run length (A first on equal prefixes: stable).  A stable sort
+// on (hi, lo) of records stored in index order IS the (hi, lo, index) order the sample sort
+// needs for its splitters.
+constexpr int TS_NT = 1024, TS_TILE = 2048;
+constexpr int MG_NT = 256, MG_CHUNK = 1024;
+
+__global__ __launch_bounds__(TS_NT) void k_tile_sort(const Rec* in, Rec* out, u64 n) {
+    __shared__ u64 sh[TS_TILE], sl[TS_TILE];
+    __shared__ uint16_t si[TS_TILE];
+    const u64 base = (u64)blockIdx.x * TS_TILE;
+    const int tid = threadIdx.x;
+    for (int k = 0; k < TS_TILE / TS_NT; k++) {
+        const int i = k * TS_NT + tid;
+        const u64 g = base + i;
+        if (g < n) {
+            const Rec r = in[g];
+            sh[i] = r.hi; sl[i] = r.lo;
+        } else {                                  // padding: no key has an all-0xFF prefix
+            sh[i] = ~0ull; sl[i] = ~0ull;
+        }
+        si[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    for (int k = 2; k <= TS_TILE; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int q = 0; q < TS_TILE / 2 / TS_NT; q++) {
+                const int t = q * TS_NT + tid;               // compare-exchange pair t
+                const int i = 2 * t - (t & (j - 1)), p = i + j;
+                const u64 ah = sh[i], al = sl[i], bh = sh[p], bl = sl[p];
+                const uint16_t ai = si[i], bi = si[p];
+                if (key3_lt(bh, bl, bi, ah, al, ai) == ((i & k) == 0)) {
+                    sh[i] = bh; sl[i] = bl; sh[p] = ah; sl[p] = al;
+                    si[i] = bi; si[p] = ai;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int k = 0; k < TS_TILE / TS_NT; k++) {
+        const int i = k * TS_NT + tid;
+        if (base + i < n) out[base + i] = in[base + si[i]];
+    }
+}
+
+// merge path: number of A records among the first d outputs of merge(A, B) (A first on equal
+// prefixes).  One wave, 64-way search: each round samples 64 split candidates.
+__device__ __forceinline__ u64 merge_split(const Rec* A, u64 la, const Rec* B, u64 lb, u64 d, int lane) {
+    u64 lo = d > lb ? d - lb : 0, hi = d < la ? d : la;
+    while (hi > lo) {
+        const u64 s = hi - lo;
+        const u64 p = s <= 64 ? lo + lane : lo + (u64)lane * s / 64;
+        bool t = false;
+        if (p < hi) {
+            const Rec& x = A[p];
+            const Rec& y = B[d - 1 - p];
+            t = !pre_lt(y.hi, y.lo, x.hi, x.lo);
+        }
+        const int c = __popcll(__ballot(t));
+        if (s <= 64) return lo + c;
+        const u64 nlo = c > 0 ? __shfl(p, c - 1) + 1 : lo;
+        const u64 nhi = c < 64 ? __shfl(p, c) : hi;
+        lo = nlo; hi = nhi;
+    }
+    return lo;
+}
+
+// merge A = in[a0, a0 + la) and B = in[a0 + la, a0 + la + lb) for the outputs [d0, d1) of that
+// pair, d1 - d0 <= 1024 (workgroup-cooperative)
+__device__ __forceinline__ void merge_block(const Rec* in, Rec* out, u64 a0, u64 la, u64 lb, u64 d0, u64 d1) {
+    __shared__ u64 sh[MG_CHUNK], sl[MG_CHUNK];
+    __shared__ u64 split[2];
+    const Rec* A = in + a0;
+    const Rec* B = A + la;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (wv < 2) {
+        const u64 sp = merge_split(A, la, B, lb, wv ? d1 : d0, lane);
+        if (lane == 0) split[wv] = sp;
+    }
+    __syncthreads();
+    const u64 i0 = split[0], i1 = split[1];
+    const u64 j0 = d0 - i0;
+    const int na = (int)(i1 - i0), m = (int)(d1 - d0);
+    Rec r[MG_CHUNK / MG_NT];
+#pragma unroll
+    for (int k = 0; k < MG_CHUNK / MG_NT; k++) {
+        const int e = k * MG_NT + tid;
+        if (e < m) {
+            r[k] = e < na ? A[i0 + e] : B[j0 + (e - na)];
+            sh[e] = r[k].hi; sl[e] = r[k].lo;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MG_CHUNK / MG_NT; k++) {
+        const int e = k * MG_NT + tid;
+        if (e >= m) continue;
+        const u64 xh = r[k].hi, xl = r[k].lo;
+        int lo, hi, pos;
+        if (e < na) {                              // B window records strictly below x
+            lo = na; hi = m;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (pre_lt(sh[mid], sl[mid], xh, xl)) lo = mid + 1; else hi = mid; }
+            pos = e + (lo - na);
+        } else {                                   // A window records at or below x
+            lo = 0; hi = na;
+            while (lo < hi) { const int mid = (lo + hi) >> 1; if (!pre_lt(xh, xl, sh[mid], sl[mid])) lo = mid + 1; else hi = mid; }
+            pos = (e - na) + lo;
+        }
+        out[a0 + d0 + pos] = r[k];
+    }
+    __syncthreads();                               // LDS reused by the caller's next pair
+}
+
+// one merge pass: runs of length w -> 2w; workgroup b writes outputs [b * 1024, +1024)
+__global__ __launch_bounds__(MG_NT) void k_merge(const Rec* in, Rec* out, u64 n, u64 w) {
+    const u64 c0 = (u64)blockIdx.x * MG_CHUNK;
+    const u64 a0 = c0 / (2 * w) * (2 * w);
+    const u64 la = n - a0 < w ? n - a0 : w;
+    const u64 rest = n - a0 - la;
+    const u64 lb = rest < w ? rest : w;
+    const u64 d0 = c0 - a0;                        // runs of 2w >= 4096 records: the chunk is
+    merge_block(in, out, a0, la, lb, d0, d0 + MG_CHUNK < la + lb ? d0 + MG_CHUNK : la + lb);   // in one pair
+}
+
+// one merge pass over runs of any length: b0[0] = 0 <= b0[1] <= ... <= b0[nr] = n are the
+// boundaries of the nr original runs; after passes of width s (1, 2, 4, ...) runs [2js, 2js + s)
+// and [2js + s, 2js + 2s) are merged.  Workgroup blk writes outputs [blk * 1024, +1024), which
+// may cover the ends of several pairs (runs of any length): it merges its part of each.
+__global__ __launch_bounds__(MG_NT) void k_merge_runs(const Rec* in, Rec* out, const u64* b0, u32 nr, u32 s) {
+    const u64 c0 = (u64)blockIdx.x * MG_CHUNK, n = b0[nr];
+    const u64 c1 = c0 + MG_CHUNK < n ? c0 + MG_CHUNK : n;
+    auto B = [&](u64 r) -> u64 { return b0[r < nr ? r : nr]; };
+    const u32 npairs = (nr + 2 * s - 1) / (2 * s);
+    u32 lo = 0, hi = npairs;                       // the last pair starting at or before c0
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) / 2;
+        if (B((u64)2 * mid * s) <= c0) lo = mid; else hi = mid;
+    }
+    for (u32 j = lo; j < npairs; j++) {            // workgroup-uniform
+        const u64 a0 = B((u64)2 * j * s), am = B((u64)2 * j * s + s), ae = B((u64)2 * j * s + 2 * s);
+        if (a0 >= c1) break;
+        if (ae <= c0 || ae == a0) continue;
+        const u64 d0 = (c0 > a0 ? c0 : a0) - a0, d1 = (c1 < ae ? c1 : ae) - a0;
+        merge_block(in, out, a0, am - a0, ae - am, d0, d1);
+    }
+}
+
+// ---------------------------------------------------------------- scans
+// exclusive scan of u64 (in place) by one workgroup of 1024 threads; total in *total
+__global__ __launch_bounds__(1024) void k_scan_u64(u64* v, u64 n, u64* total) {
+    __shared__ u64 ws[16];
+    __shared__ u64 carry_s;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) carry_s = 0;
+    __syncthreads();
+    for (u64 base = 0; base < n; base += 1024 * 4) {
+        u64 x[4], s = 0;
+        for (int k = 0; k < 4; k++) {
+            u64 i = base + (u64)tid * 4 + k;
+            x[k] = i < n ? v[i] : 0;
+            s += x[k];
+        }
+        u64 incl = s;
+        for (int d = 1; d < 64; d <<= 1) { u64 y = __shfl_up(incl, d, 64); if (lane >= d) incl += y; }
+        if (lane == 63) ws[w] = incl;
+        __syncthreads();
+        u64 wpre = 0, all = 0;
+        for (int k = 0; k < 16; k++) { if (k < w) wpre += ws[k]; all += ws[k]; }
+        u64 run = carry_s + wpre + incl - s;
+        for (int k = 0; k < 4; k++) {
+            u64 i = base + (u64)tid * 4 + k;
+            if (i < n) v[i] = run;
+            run += x[k];
+        }
+        __syncthreads();
+        if (tid == 0) carry_s += all;
+        __syncthreads();
+    }
+    if (tid == 0 && total) *total = carry_s;
+}
+
+// multi-block exclusive scan of u32 (in place): k_scan_part sums SC_SEG-element segments into
+// part[], k_scan_u64 scans part[], k_scan_apply scans each segment from its base
+constexpr int SC_NT = 1024, SC_IPT = 8, SC_SEG = SC_NT * SC_IPT;
+
+__device__ __forceinline__ u64 block_sum_u64(u64 s, u64* ws) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+    if (lane == 0) ws[w] = s;
+    __syncthreads();
+    u64 all = 0;
+    for (int k = 0; k < (int)(blockDim.x / 64); k++) all += ws[k];
+    __syncthreads();
+    return all;
+}
+
+__global__ __launch_bounds__(SC_NT) void k_scan_part(const u32* v, u64 n, u64* part) {
+    __shared__ u64 ws[SC_NT / 64];
+    const u64 base = (u64)blockIdx.x * SC_SEG;
+    u64 s = 0;
+#pragma unroll
+    for (int k = 0; k < SC_IPT; k++) {
+        const u64 i = base + (u64)k * SC_NT + threadIdx.x;
+        s += i < n ? v[i] : 0u;
+    }
+    const u64 all = block_sum_u64(s, ws);
+    if (threadIdx.x == 0) part[blockIdx.x] = all;
+}
+
+__global__ __launch_bounds__(SC_NT) void k_scan_apply(u32* v, u64 n, const u64* part) {
+    __shared__ u64 ws[SC_NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u64 base = (u64)blockIdx.x * SC_SEG + (u64)tid * SC_IPT;   // consecutive per thread
+    u32 x[SC_IPT];
+    u64 s = 0;
+#pragma unroll
+    for (int k = 0; k < SC_IPT; k++) { x[k] = base + k < n ? v[base + k] : 0u; s += x[k]; }
+    u64 incl = s;
+    for (int d = 1; d < 64; d <<= 1) { const u64 y = __shfl_up(incl, d, 64); if (lane >= d) incl += y; }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    u64 pre = 0;
+    for (int k = 0; k < w; k++) pre += ws[k];
+    u64 run = part[blockIdx.x] + pre + incl - s;
+#pragma unroll
+    for (int k = 0; k < SC_IPT; k++) {
+        if (base + k < n) v[base + k] = (u32)run;
+        run += x[k];
+    }
+}
+
+// ---------------------------------------------------------------- sample sort
+constexpr u32 SS_TARGET = 2048;        // expected records per bucket
+constexpr u32 SS_CAP = 4096;           // bucket size sorted in LDS (larger: the global path)
+constexpr u32 SS_OVS = 16;             // samples per bucket
+constexpr u32 SS_MAXB = 32768;         // buckets (k_ss_hist / k_ss_scatter LDS: 4 B each)
+constexpr int SS_NT = 256;             // hist / scatter workgroups
+constexpr int SB_NT = 1024;            // bucket sort workgroups
+
+struct SortArgs {
+    const Rec* rec;          // compacted records (index = position)
+    u64 n;
+    const Rec* smp;          // sorted sample: hi, lo, cnt = record index
+    u64 S;                   // samples
+    u32 B;                   // buckets
+    u32 G;                   // hist/scatter workgroups
+    u32* bid;                // bucket of every record
+    u32* hist;               // [B][G] counts -> exclusive offsets (bucket-major)
+    uint4* ikey;             // items by bucket: {lo.x, lo.y, hi.x, hi.y} (hi, lo)
+    u32* iidx;               // record index of each item
+    uint4* ikey2;            // scratch of the global (oversized bucket) path
+    u32* iidx2;
+    Rec* out;                // sorted records
+};
+
+// sample j = record floor(j * n / S): stored in index order, so a stable sort gives the
+// (hi, lo, index) order
+__global__ void k_ss_sample(SortArgs a, Rec* smp) {
+    const u64 j = blockIdx.x * (u64)blockDim.x + threadIdx.x;
+    if (j >= a.S) return;
+    const u64 i = j * a.n / a.S;
+    const Rec r = a.rec[i];
+    Rec s;
+    s.hi = r.hi; s.lo = r.lo; s.cnt = i; s.ref = 0;
+    smp[j] = s;
+}
+
+// splitter b (0 <= b < B - 1) = sample (b + 1) * S / B; bucket(x) = number of splitters <= x
+__device__ __forceinline__ u32 ss_bucket(const SortArgs& a, u64 hi, u64 lo, u32 idx) {
+    u32 l = 0, h = a.B - 1;
+    while (l < h) {
+        const u32 mid = (l + h) >> 1;
+        const Rec& s = a.smp[(u64)(mid + 1) * a.S / a.B];
+        if (!key3_lt(hi, lo, idx, s.hi, s.lo, (u32)s.cnt)) l = mid + 1; else h = mid;
+    }
+    return l;
+}
+
+__device__ __forceinline__ void ss_range(const SortArgs& a, u64& i0, u64& i1) {
+    i0 = a.n * blockIdx.x / a.G;
+    i1 = a.n * (blockIdx.x + 1) / a.G;
+}
+
+__global__ __launch_bounds__(SS_NT) void k_ss_hist(SortArgs a) {
+    __shared__ u32 h[SS_MAXB];
+    for (u32 b = threadIdx.x; b < a.B; b += SS_NT) h[b] = 0;
+    __syncthreads();
+    u64 i0, i1;
+    ss_range(a, i0, i1);
+    for (u64 i = i0 + threadIdx.x; i < i1; i += SS_NT) {
+        const Rec r = a.rec[i];
+        const u32 b = ss_bucket(a, r.hi, r.lo, (u32)i);
+        a.bid[i] = b;
+        atomicAdd(&h[b], 1u);
+    }
+    __syncthreads();
+    for (u32 b = threadIdx.x; b < a.B; b += SS_NT) a.hist[(u64)b * a.G + blockIdx.x] = h[b];
+}
+
+// items of workgroup g go to [hist[b][g], ...) of their bucket; the order inside a bucket does
+// not matter (the bucket sort orders by (hi, lo, index) completely)
+__global__ __launch_bounds__(SS_NT) void k_ss_scatter(SortArgs a) {
+    __shared__ u32 cur[SS_MAXB];
+    for (u32 b = threadIdx.x; b < a.B; b += SS_NT) cur[b] = a.hist[(u64)b * a.G + blockIdx.x];
+    __syncthreads();
+    u64 i0, i1;
+    ss_range(a, i0, i1);
+    for (u64 i = i0 + threadIdx.x; i < i1; i += SS_NT) {
+        const Rec r = a.rec[i];
+        const u32 d = atomicAdd(&cur[a.bid[i]], 1u);
+        a.ikey[d] = make_uint4((u32)r.lo, (u32)(r.lo >> 32), (u32)r.hi, (u32)(r.hi >> 32));
+        a.iidx[d] = (u32)i;
+    }
+}
+
+__device__ __forceinline__ u64 ik_hi(uint4 k) { return (u64)k.w << 32 | k.z; }
+__device__ __forceinline__ u64 ik_lo(uint4 k) { return (u64)k.y << 32 | k.x; }
+
+// Oversized bucket (more than SS_CAP records: only when sampling was unlucky, or SS_TARGET was
+// forced up for a test): the workgroup sorts [s, s + m) of the item arrays through global
+// memory - LDS-sorted chunks of SS_CAP, then pairwise merge passes (ping-pong with ikey2/iidx2),
+// each pass split over the threads by merge-path partitions.  Returns the array holding the
+// result (0: ikey/iidx, 1: ikey2/iidx2).
+__device__ int ss_global_sort(const SortArgs& a, u64 s, u64 m, u64* sk_hi, u64* sk_lo, u32* sk_i) {
+    const int tid = threadIdx.x;
+    for (u64 c0 = 0; c0 < m; c0 += SS_CAP) {         // LDS bitonic per chunk
+        const u32 cm = (u32)(m - c0 < SS_CAP ? m - c0 : SS_CAP);
+        for (u32 e = tid; e < SS_CAP; e += SB_NT) {
+            if (e < cm) {
+                const uint4 k = a.ikey[s + c0 + e];
+                sk_hi[e] = ik_hi(k); sk_lo[e] = ik_lo(k); sk_i[e] = a.iidx[s + c0 + e];
+            } else { sk_hi[e] = ~0ull; sk_lo[e] = ~0ull; sk_i[e] = ~0u; }
+        }
+        __syncthreads();
+        for (u32 k = 2; k <= SS_CAP; k <<= 1)
+            for (u32 j = k >> 1; j > 0; j >>= 1) {
+                for (u32 t = tid; t < SS_CAP / 2; t += SB_NT) {
+                    const u32 i = 2 * t - (t & (j - 1)), p = i + j;
+                    if (key3_lt(sk_hi[p], sk_lo[p], sk_i[p], sk_hi[i], sk_lo[i], sk_i[i]) == ((i & k) == 0)) {
+                        u64 x = sk_hi[i]; sk_hi[i] = sk_hi[p]; sk_hi[p] = x;
+                        x = sk_lo[i]; sk_lo[i] = sk_lo[p]; sk_lo[p] = x;
+                        const u32 y = sk_i[i]; sk_i[i] = sk_i[p]; sk_i[p] = y;
+                    }
+                }
+                __syncthreads();
+            }
+        for (u32 e = tid; e < cm; e += SB_NT) {
+            a.ikey[s + c0 + e] = make_uint4((u32)sk_lo[e], (u32)(sk_lo[e] >> 32), (u32)sk_hi[e], (u32)(sk_hi[e] >> 32));
+            a.iidx[s + c0 + e] = sk_i[e];
+        }
+        __syncthreads();
+    }
+    int src = 0;
+    for (u64 w = SS_CAP; w < m; w *= 2) {
+        const uint4* KI = src ? a.ikey2 : a.ikey;
+        const u32* II = src ? a.iidx2 : a.iidx;
+        uint4* KO = src ? a.ikey : a.ikey2;
+        u32* IO = src ? a.iidx : a.iidx2;
+        for (u64 p0 = 0; p0 < m; p0 += 2 * w) {
+            const u64 la = m - p0 < w ? m - p0 : w;
+            const u64 lb = m - p0 - la < w ? m - p0 - la : w;
+            const u64 L = la + lb;
+            const u64 A = s + p0, Bq = s + p0 + la;
+            // thread t writes outputs [t * L / SB_NT, (t + 1) * L / SB_NT)
+            const u64 d0 = L * tid / SB_NT, d1 = L * (tid + 1) / SB_NT;
+            auto lt_at = [&](u64 x, u64 y) -> bool {       // item x (in B) < item y (in A)?
+                const uint4 kx = KI[x], ky = KI[y];
+                return key3_lt(ik_hi(kx), ik_lo(kx), II[x], ik_hi(ky), ik_lo(ky), II[y]);
+            };
+            u64 lo = d0 > lb ? d0 - lb : 0, hi = d0 < la ? d0 : la;   // #A among the first d0
+            while (lo < hi) {
+                const u64 mid = (lo + hi) >> 1;
+                if (lt_at(Bq + (d0 - 1 - mid), A + mid)) hi = mid; else lo = mid + 1;
+            }
+            u64 ia = lo, ib = d0 - lo;
+            for (u64 d = d0; d < d1; d++) {
+                bool takeA;
+                if (ia >= la) takeA = false;
+                else if (ib >= lb) takeA = true;
+                else takeA = !lt_at(Bq + ib, A + ia);
+                const u64 q = takeA ? A + ia : Bq + ib;
+                KO[s + p0 + d] = KI[q];
+                IO[s + p0 + d] = II[q];
+                if (takeA) ia++; else ib++;
+            }
+        }
+        __syncthreads();
+        src ^= 1;
+    }
+    return src;
+}
+
+// one workgroup per bucket: bitonic sort of (hi, lo, index) in LDS, then gather the records
+__global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
+    __shared__ u64 sk_hi[SS_CAP], sk_lo[SS_CAP];
+    __shared__ u32 sk_i[SS_CAP];
+    const u32 b = blockIdx.x;
+    const u64 s = a.hist[(u64)b * a.G];
+    const u64 e = b + 1 < a.B ? a.hist[(u64)(b + 1) * a.G] : a.n;
+    const u64 m = e - s;
+    const int tid = threadIdx.x;
+    if (m == 0) return;
+    if (m > SS_CAP) {
+        const int src = ss_global_sort(a, s, m, sk_hi, sk_lo, sk_i);
+        const u32* II = src ? a.iidx2 : a.iidx;
+        for (u64 j = tid; j < m; j += SB_NT) a.out[s + j] = a.rec[II[s + j]];
+        return;
+    }
+    u32 P = 64;
+    while (P < m) P <<= 1;
+    for (u32 j = tid; j < P; j += SB_NT) {
+        if (j < m) {
+            const uint4 k = a.ikey[s + j];
+            sk_hi[j] = ik_hi(k); sk_lo[j] = ik_lo(k); sk_i[j] = a.iidx[s + j];
+        } else { sk_hi[j] = ~0ull; sk_lo[j] = ~0ull; sk_i[j] = ~0u; }
+    }
+    __syncthreads();
+    for (u32 k = 2; k <= P; k <<= 1)
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+            for (u32 t = tid; t < P / 2; t += SB_NT) {
+                const u32 i = 2 * t - (t & (j - 1)), p = i + j;
+                const u64 ah = sk_hi[i], al = sk_lo[i], bh = sk_hi[p], bl = sk_lo[p];
+                const u32 ai = sk_i[i], bi = sk_i[p];
+                if (key3_lt(bh, bl, bi, ah, al, ai) == ((i & k) == 0)) {
+                    sk_hi[i] = bh; sk_lo[i] = bl; sk_i[i] = bi;
+                    sk_hi[p] = ah; sk_lo[p] = al; sk_i[p] = ai;
+                }
+            }
+            __syncthreads();
+        }
+    for (u32 j = tid; j < m; j += SB_NT) a.out[s + j] = a.rec[sk_i[j]];
+}
+
+// ---------------------------------------------------------------- tie groups
+// A record's key bytes: inline keys are their prefix; a long key (ref & LONG_FLAG) lives at
+// base + (ref & LONG_OFF_MASK), (ref >> 40) & LONG_LEN_MAX bytes - base is the long-key arena
+// (zero-padded 16-byte cells) or, for merged runs, the formatted text (any alignment).
+__device__ __forceinline__ bool rec_long(const Rec& r) { return (r.ref & LONG_FLAG) != 0; }
+__device__ __forceinline__ u64 key_bytes_len(const Rec& r) { return (r.ref >> 40) & LONG_LEN_MAX; }
+
+// big-endian 8 bytes of key x from byte k on (zeros past its end)
+__device__ __forceinline__ u64 key_word_be(const uint8_t* base, const Rec& r, u64 k) {
+    const u64 len = key_bytes_len(r);
+    const uint8_t* p = base + (r.ref & LONG_OFF_MASK);
+    u64 v = 0;
+    for (int q = 0; q < 8; q++) v = (v << 8) | (k + q < len ? p[k + q] : 0u);
+    return v;
+}
+
+// full bytewise order of two long keys with equal first 32 bytes (the slow path of the tie sort)
+__device__ int key_cmp_from(const uint8_t* base, const Rec& x, const Rec& y, u64 from) {
+    const u64 lx = key_bytes_len(x), ly = key_bytes_len(y);
+    const uint8_t* px = base + (x.ref & LONG_OFF_MASK);
+    const uint8_t* py = base + (y.ref & LONG_OFF_MASK);
+    const u64 m = lx < ly ? lx : ly;
+    for (u64 i = from; i < m; i++)
+        if (px[i] != py[i]) return px[i] < py[i] ? -1 : 1;
+    return lx < ly ? -1 : (lx > ly ? 1 : 0);
+}
+
+__device__ __forceinline__ bool same_prefix(const Rec& x, const Rec& y) { return x.hi == y.hi && x.lo == y.lo; }
+
+// group starts: long keys whose successor shares their 16-byte prefix and whose predecessor
+// does not
+__global__ void k_tie_mark(const Rec* r, u64 n, u64* groups, u64* ngroups) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i + 1 < n; i += (u64)gridDim.x * blockDim.x) {
+        const Rec x = r[i], y = r[i + 1];
+        if (!rec_long(x) || !rec_long(y) || !same_prefix(x, y)) continue;
+        if (i > 0) {
+            const Rec w = r[i - 1];
+            if (rec_long(w) && same_prefix(w, x)) continue;
+        }
+        groups[atomicAdd(ngroups, 1ull)] = i;
+    }
+}
+
+// One workgroup per group (grid-stride over the group list): the group's extent, then a
+// bitonic sort by (bytes 16-31, then the full key from byte 32, slow path), in LDS up to
+// TG_CAP records, through scratch (2 * start, padded to a power of two) beyond that; the
+// records are permuted through `tmp` (the compacted array, free by then).
+constexpr int TG_NT = 1024;
+constexpr u32 TG_CAP = 2048;
+
+struct TieArgs {
+    Rec* r;                // sorted records
+    u64 n;
+    const uint8_t* base;   // key bytes of long records
+    const u64* groups;
+    const u64* ngroups;
+    Rec* tmp;              // >= n records
+    uint4* sc_key;         // >= 2n scratch items (bytes 16-31 big-endian) ...
+    u32* sc_pos;           // ... and the record position
+};
+
+__device__ __forceinline__ bool tie_lt(const TieArgs& a, u64 xh, u64 xl, u32 xp, u64 yh, u64 yl, u32 yp) {
+    if (xh != yh) return xh < yh;
+    if (xl != yl) return xl < yl;
+    if (xp == yp) return false;
+    if (xp == ~0u || yp == ~0u) return yp == ~0u;     // padding sorts last
+    return key_cmp_from(a.base, a.r[xp], a.r[yp], 32) < 0;
+}
+
+__global__ __launch_bounds__(TG_NT) void k_tie_sort(TieArgs a) {
+    __shared__ u64 th[TG_CAP], tl[TG_CAP];
+    __shared__ u32 tp[TG_CAP];
+    __shared__ u64 end_s;
+    const int tid = threadIdx.x;
+    const u64 ng = *a.ngroups;
+    for (u64 g = blockIdx.x; g < ng; g += gridDim.x) {
+        const u64 s = a.groups[g];
+        const Rec x0 = a.r[s];
+        // extent: the first record past s that is short or has another prefix, 1024 at a time
+        if (tid == 0) end_s = a.n;
+        __syncthreads();
+        for (u64 base = s + 1; base < a.n; base += TG_NT) {
+            const u64 i = base + tid;
+            bool stop = false;
+            if (i < a.n) { const Rec y = a.r[i]; stop = !rec_long(y) || !same_prefix(x0, y); }
+            if (stop) atomicMin((unsigned long long*)&end_s, (unsigned long long)i);
+            __syncthreads();
+            const u64 e = end_s;
+            __syncthreads();
+            if (e < a.n) break;
+        }
+        const u64 m = end_s - s;
+        if (m <= TG_CAP) {
+            u32 P = 2;
+            while (P < m) P <<= 1;
+            for (u32 j = tid; j < P; j += TG_NT) {
+                if (j < m) {
+                    const Rec y = a.r[s + j];
+                    th[j] = key_word_be(a.base, y, 16); tl[j] = key_word_be(a.base, y, 24); tp[j] = (u32)(s + j);
+                } else { th[j] = ~0ull; tl[j] = ~0ull; tp[j] = ~0u; }
+            }
+            __syncthreads();
+            for (u32 k = 2; k <= P; k <<= 1)
+                for (u32 j = k >> 1; j > 0; j >>= 1) {
+                    for (u32 t = tid; t < P / 2; t += TG_NT) {
+                        const u32 i = 2 * t - (t & (j - 1)), p = i + j;
+                        if (tie_lt(a, th[p], tl[p], tp[p], th[i], tl[i], tp[i]) == ((i & k) == 0)) {
+                            u64 v = th[i]; th[i] = th[p]; th[p] = v;
+                            v = tl[i]; tl[i] = tl[p]; tl[p] = v;
+                            const u32 q = tp[i]; tp[i] = tp[p]; tp[p] = q;
+                        }
+                    }
+                    __syncthreads();
+                }
+            for (u32 j = tid; j < m; j += TG_NT) a.tmp[s + j] = a.r[tp[j]];
+        } else {
+            u64 P = 2;
+            while (P < m) P <<= 1;
+            uint4* K = a.sc_key + 2 * s;
+            u32* Q = a.sc_pos + 2 * s;
+            for (u64 j = tid; j < P; j += TG_NT) {
+                if (j < m) {
+                    const Rec y = a.r[s + j];
+                    const u64 h = key_word_be(a.base, y, 16), l = key_word_be(a.base, y, 24);
+                    K[j] = make_uint4((u32)l, (u32)(l >> 32), (u32)h, (u32)(h >> 32));
+                    Q[j] = (u32)(s + j);
+                } else { K[j] = make_uint4(~0u, ~0u, ~0u, ~0u); Q[j] = ~0u; }
+            }
+            __syncthreads();
+            for (u64 k = 2; k <= P; k <<= 1)
+                for (u64 j = k >> 1; j > 0; j >>= 1) {
+                    for (u64 t = tid; t < P / 2; t += TG_NT) {
+                        const u64 i = 2 * t - (t & (j - 1)), p = i + j;
+                        const uint4 ki = K[i], kp = K[p];
+                        const u32 qi = Q[i], qp = Q[p];
+                        if (tie_lt(a, ik_hi(kp), ik_lo(kp), qp, ik_hi(ki), ik_lo(ki), qi) == ((i & k) == 0)) {
+                            K[i] = kp; K[p] = ki; Q[i] = qp; Q[p] = qi;
+                        }
+                    }
+                    __syncthreads();
+                }
+            for (u64 j = tid; j < m; j += TG_NT) a.tmp[s + j] = a.r[Q[j]];
+        }
+        __syncthreads();
+        for (u64 j = tid; j < m; j += TG_NT) a.r[s + j] = a.tmp[s + j];
+        __syncthreads();
+    }
+}
+
+}  // namespace wcg

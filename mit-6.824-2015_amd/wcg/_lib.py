@@ -23,7 +23,8 @@ EXPORTED = [
     "wcg_open", "wcg_close", "wcg_last_error", "wcg_set_stream", "wcg_reset", "wcg_map",
     "wcg_map_device", "wcg_reduce", "wcg_result_device", "wcg_result_copy", "wcg_partition",
     "wcg_export", "wcg_import", "wcg_timings", "wcg_enable_timing", "wcg_stats", "wcg_ihash",
-    "wcg_version",
+    "wcg_version", "wcg_map_file", "wcg_partition_all", "wcg_map_json", "wcg_export_count",
+    "wcg_export_write", "wcg_merge_runs", "wcg_result_copy_device", "wcg_sync",
 ]
 
 
@@ -63,6 +64,14 @@ def load() -> ctypes.CDLL:
         "wcg_stats": (I, [P, PU64]),
         "wcg_ihash": (U32, [ctypes.c_char_p, U64]),
         "wcg_version": (ctypes.c_char_p, []),
+        "wcg_map_file": (I, [P, ctypes.c_char_p, PU64, PU64]),
+        "wcg_partition_all": (I, [P, U32, P, U64, PU64]),
+        "wcg_map_json": (I, [P, ctypes.c_char_p, U64, U32, P, U64, PU64]),
+        "wcg_export_count": (I, [P, U32, U32, PU64]),
+        "wcg_export_write": (I, [P, P]),
+        "wcg_merge_runs": (I, [P, P, PU64, U32, PU64, PU64]),
+        "wcg_result_copy_device": (I, [P, P]),
+        "wcg_sync": (I, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -164,6 +173,22 @@ class Engine:
     def map_device(self, dev_ptr: int, n: int) -> None:
         self._chk(self._lib.wcg_map_device(self._ctx, ctypes.c_void_p(dev_ptr), n))
 
+    def map_file(self, path: str) -> Tuple[int, int]:
+        """Split + DoMap of a whole file through the pinned double-buffered ingest; returns
+        (bytes mapped, file size) - fewer bytes mapped when a 64 KiB+ line ended the scan (P1)."""
+        mapped, size = ctypes.c_uint64(), ctypes.c_uint64()
+        self._chk(self._lib.wcg_map_file(self._ctx, os.fsencode(path), ctypes.byref(mapped), ctypes.byref(size)))
+        return mapped.value, size.value
+
+    def map_json(self, data: bytes, nreduce: int) -> List[bytes]:
+        """DoMap's reference-exact JSON intermediate files (one per partition) for one split."""
+        sizes = (ctypes.c_uint64 * nreduce)()
+        self._chk(self._lib.wcg_map_json(self._ctx, data, len(data), nreduce, None, 0, sizes))
+        total = sum(sizes)
+        buf = ctypes.create_string_buffer(max(total, 1))
+        self._chk(self._lib.wcg_map_json(self._ctx, data, len(data), nreduce, buf, total, sizes))
+        return _slices(buf.raw, list(sizes))
+
     def reduce(self) -> Tuple[int, int]:
         nk, nb = ctypes.c_uint64(), ctypes.c_uint64()
         self._chk(self._lib.wcg_reduce(self._ctx, ctypes.byref(nk), ctypes.byref(nb)))
@@ -174,11 +199,27 @@ class Engine:
         self._chk(self._lib.wcg_result_device(self._ctx, ctypes.byref(p), ctypes.byref(nb)))
         return p.value or 0, nb.value
 
+    def result_copy_device(self, dev_ptr: int) -> None:
+        """Async device copy of the formatted output into a caller's buffer (context stream)."""
+        self._chk(self._lib.wcg_result_copy_device(self._ctx, ctypes.c_void_p(dev_ptr)))
+
+    def sync(self) -> None:
+        self._chk(self._lib.wcg_sync(self._ctx))
+
     def result(self) -> bytes:
         _, nb = self.result_device()
         buf = ctypes.create_string_buffer(max(nb, 1))
         self._chk(self._lib.wcg_result_copy(self._ctx, buf, nb))
         return buf.raw[:nb]
+
+    def partitions(self, nreduce: int) -> List[bytes]:
+        """Every -res-<r> file of the last reduce (one device formatting pass for all)."""
+        sizes = (ctypes.c_uint64 * nreduce)()
+        self._chk(self._lib.wcg_partition_all(self._ctx, nreduce, None, 0, sizes))
+        total = sum(sizes)
+        buf = ctypes.create_string_buffer(max(total, 1))
+        self._chk(self._lib.wcg_partition_all(self._ctx, nreduce, buf, total, sizes))
+        return _slices(buf.raw, list(sizes))
 
     def partition(self, nreduce: int, r: int) -> bytes:
         nb = ctypes.c_uint64()
@@ -194,8 +235,27 @@ class Engine:
         self._chk(self._lib.wcg_export(self._ctx, nreduce, nranks, ctypes.byref(p), counts))
         return p.value or 0, list(counts)
 
+    def export_count(self, nreduce: int, nranks: int) -> List[int]:
+        """Units per destination rank of the local aggregate (one host synchronisation)."""
+        counts = (ctypes.c_uint64 * nranks)()
+        self._chk(self._lib.wcg_export_count(self._ctx, nreduce, nranks, counts))
+        return list(counts)
+
+    def export_write(self, dev_ptr: int) -> None:
+        """Write the units counted by export_count into a caller's device buffer (async)."""
+        self._chk(self._lib.wcg_export_write(self._ctx, ctypes.c_void_p(dev_ptr)))
+
     def import_records(self, dev_ptr: int, nunits: int) -> None:
         self._chk(self._lib.wcg_import(self._ctx, ctypes.c_void_p(dev_ptr), nunits))
+
+    def merge_runs(self, dev_ptr: int, run_bytes: List[int]) -> Tuple[int, int]:
+        """Merge sorted "key: count\n" runs held back to back at dev_ptr into this context's
+        result (Merge, mapreduce.go:284-321); returns (keys, bytes)."""
+        rb = (ctypes.c_uint64 * max(len(run_bytes), 1))(*run_bytes)
+        nk, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        self._chk(self._lib.wcg_merge_runs(self._ctx, ctypes.c_void_p(dev_ptr), rb, len(run_bytes),
+                                           ctypes.byref(nk), ctypes.byref(nb)))
+        return nk.value, nb.value
 
     # -- host copies of the record units (the file-based shuffle of the config-5 workers)
     def export_host(self, nreduce: int, nranks: int) -> Tuple[bytes, List[int]]:
@@ -240,6 +300,14 @@ class Engine:
         keys = ["tokens", "keys", "lds_hits", "global_ops", "long_tokens", "arena_bytes", "overflow",
                 "spin_fail"]
         return dict(zip(keys, list(s)))
+
+
+def _slices(raw: bytes, sizes: List[int]) -> List[bytes]:
+    out, off = [], 0
+    for n in sizes:
+        out.append(raw[off:off + n])
+        off += n
+    return out
 
 
 def version() -> str:

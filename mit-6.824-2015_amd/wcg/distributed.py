@@ -8,11 +8,13 @@ Here each rank maps a line-aligned byte range (rank = a group of map jobs), pre-
 (key, count) on its GPU, exports its records bucketed by owner = (ihash % nReduce) % world
 (partition r is owned by rank r % world), and one all_to_all_single (RCCL grouped
 send/recv over xGMI) delivers every partition to its owner, which reduces it (= DoReduce for
-its partitions).  The final Merge gathers the owners' disjoint results on rank 0.
+its partitions: sort + format).  The final Merge sends the owners' sorted runs to rank 0, which
+merges them on its GPU (k-way, by pairwise merge passes).
 
-The module is device-agnostic: it only needs an engine with export_tensor/import_tensor/
-reset/reduce/result, so the CPU tests drive it with the `gloo` backend and an oracle-backed
-stand-in engine (tests/test_distributed.py); the product engine is wcg.Engine.
+The module is device-agnostic: it only needs an engine with export_tensor/import_tensor/reset/
+reduce/result/result_tensor/merge_runs_tensor, so the CPU tests drive it with the `gloo` backend
+and an oracle-backed stand-in engine (tests/test_distributed.py); the product engine is
+wcg.Engine wrapped in TorchEngine.
 """
 from __future__ import annotations
 
@@ -72,25 +74,27 @@ def line_aligned_ranges(total: int, world: int, byte_at) -> List[Tuple[int, int]
 
 
 # ---------------------------------------------------------------- the shuffle
-def _exchange(send: torch.Tensor, send_units: List[int], group=None) -> Tuple[torch.Tensor, List[int]]:
-    """all-to-all-v of 32-byte record units.  Counts first (small all_to_all), then payload."""
+def _exchange(send: torch.Tensor, send_units: List[int], group=None, unit: int = RECORD_BYTES
+              ) -> Tuple[torch.Tensor, List[int]]:
+    """all-to-all-v of `unit`-byte items.  Counts first (small all_to_all), then payload."""
     world = dist.get_world_size(group)
     dev = send.device
     sc = torch.tensor(send_units, dtype=torch.int64, device=dev)
     rc = torch.empty(world, dtype=torch.int64, device=dev)
     dist.all_to_all_single(rc, sc, group=group)
     recv_units = [int(x) for x in rc.tolist()]
-    recv = torch.empty(max(sum(recv_units), 1) * RECORD_BYTES, dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(recv[: sum(recv_units) * RECORD_BYTES], send[: sum(send_units) * RECORD_BYTES],
-                           output_split_sizes=[u * RECORD_BYTES for u in recv_units],
-                           input_split_sizes=[u * RECORD_BYTES for u in send_units], group=group)
+    recv = torch.empty(max(sum(recv_units), 1) * unit, dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(recv[: sum(recv_units) * unit], send[: sum(send_units) * unit],
+                           output_split_sizes=[u * unit for u in recv_units],
+                           input_split_sizes=[u * unit for u in send_units], group=group)
     return recv, recv_units
 
 
 def shuffle(engine, nreduce: int, group=None) -> None:
-    """The ihash shuffle: export the local aggregate by owner, all-to-all it, and import what
-    this rank owns.  Afterwards `engine` holds exactly the (aggregated) keys of the partitions
-    this rank owns (mapreduce.go:214-223 partitioning, :242-263 gathering)."""
+    """The ihash shuffle: export the local aggregate by owner straight into the send buffer,
+    all-to-all it, and import what this rank owns.  Afterwards `engine` holds exactly the
+    (aggregated) keys of the partitions this rank owns (mapreduce.go:214-223 partitioning,
+    :242-263 gathering)."""
     world = dist.get_world_size(group)
     send, units = engine.export_tensor(nreduce, world)
     recv, rcv_units = _exchange(send, units, group)
@@ -99,43 +103,50 @@ def shuffle(engine, nreduce: int, group=None) -> None:
 
 
 def shuffle_reduce(engine, nreduce: int, group=None) -> int:
-    """shuffle(), then DoReduce for the owned partitions (sorted and formatted on this rank).
-    Returns the number of keys this rank owns."""
+    """shuffle(), then DoReduce for the owned partitions: this rank sorts and formats its keys
+    (its sorted run of the final Merge).  Returns the number of keys this rank owns."""
     shuffle(engine, nreduce, group)
     nkeys, _ = engine.reduce()
     return nkeys
 
 
-def gather_merge(engine, root_engine, root: int = 0, group=None, fetch: bool = True) -> Optional[bytes]:
-    """Merge (mapreduce.go:284-321) across ranks: every owner sends its keys to `root`, whose
-    engine re-sorts the union (the owners' key sets are disjoint).  Returns the merged file
-    bytes on root (fetch=False: leaves them in root_engine's device buffer and returns b""),
-    None elsewhere."""
+def gather_merge(engine, root: int = 0, group=None, fetch: bool = True) -> Optional[bytes]:
+    """Merge (mapreduce.go:284-321) across ranks, after shuffle_reduce: every owner sends its
+    sorted run (its formatted "key: count\n" output; the owners' key sets are disjoint) to
+    `root`, which merges the runs on its GPU (wcg_merge_runs: ceil(log2 world) merge passes, no
+    re-sort).  Returns the merged file bytes on root (fetch=False: leaves them in the root
+    engine's device buffer and returns b""), None elsewhere."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    send, units = engine.export_tensor(1, 1)
-    n = units[0]
+    send, nbytes = engine.result_tensor()
     sizes = [0] * world
-    sizes[root] = n
-    recv, rcv_units = _exchange(send, sizes, group)
+    sizes[root] = nbytes
+    recv, run_bytes = _exchange(send, sizes, group, unit=1)
     if rank != root:
         return None
-    root_engine.reset()
-    root_engine.import_tensor(recv, sum(rcv_units))
-    root_engine.reduce()
-    return root_engine.result() if fetch else b""
+    engine.merge_runs_tensor(recv, run_bytes)
+    return engine.result() if fetch else b""
 
 
 class TorchEngine:
     """wcg.Engine + torch buffers for the collectives (device memory stays in HBM).
 
-    host_staging=True hands the collectives host tensors instead (for the gloo backend, e.g.
-    several ranks sharing one GPU in a test; RCCL needs one GPU per rank)."""
+    The engine is bound to torch's current stream (when that is not the legacy default stream),
+    so the export kernels, the collectives and the import kernels are ordered on one stream with
+    no host waits between them.  On the default stream the engine keeps its own stream and every
+    hand-over synchronises instead.  host_staging=True hands the collectives host tensors (for
+    the gloo backend, e.g. several ranks sharing one GPU in a test; RCCL needs one GPU per rank).
+    """
 
-    def __init__(self, engine, stream_ptr: int = 0, host_staging: bool = False):
+    def __init__(self, engine, stream_ptr: Optional[int] = None, host_staging: bool = False):
         self.e = engine
-        self.stream = stream_ptr
         self.host_staging = host_staging
+        cur = torch.cuda.current_stream().cuda_stream
+        if stream_ptr is None:
+            stream_ptr = cur
+        if stream_ptr:
+            engine.set_stream(stream_ptr)
+        self.ordered = bool(stream_ptr) and stream_ptr == cur
 
     def reset(self):
         self.e.reset()
@@ -146,17 +157,42 @@ class TorchEngine:
     def result(self):
         return self.e.result()
 
+    def _before_engine(self):            # torch's writes (copies, collectives) land first
+        if not self.ordered:
+            torch.cuda.current_stream().synchronize()
+
+    def _after_engine(self):             # the engine's writes / reads of a torch buffer are done
+        if not self.ordered:
+            self.e.sync()
+
     def export_tensor(self, nreduce: int, nranks: int):
-        ptr, counts = self.e.export(nreduce, nranks)
+        counts = self.e.export_count(nreduce, nranks)
         total = sum(counts)
         t = torch.empty(max(total, 1) * RECORD_BYTES, dtype=torch.uint8, device="cuda")
-        device_copy(t.data_ptr(), ptr, total * RECORD_BYTES, self.stream)
-        torch.cuda.current_stream().synchronize()
+        self._before_engine()
+        self.e.export_write(t.data_ptr())          # the send buffer itself: no extra copy
+        self._after_engine()
         return (t.cpu() if self.host_staging else t), counts
 
     def import_tensor(self, t: torch.Tensor, nunits: int):
         if not t.is_cuda:
             t = t.to("cuda")
-        torch.cuda.current_stream().synchronize()
+        self._before_engine()
         self.e.import_records(t.data_ptr(), nunits)
-        torch.cuda.current_stream().synchronize()     # t may be freed on return
+        self._after_engine()                     # ordered: t's memory is reused only after the import
+
+    def result_tensor(self):
+        """This rank's formatted output as a tensor (one device copy of at most a few MB per
+        rank at the configs' vocabularies)."""
+        _, nb = self.e.result_device()
+        t = torch.empty(max(nb, 1), dtype=torch.uint8, device="cuda")
+        self._before_engine()
+        self.e.result_copy_device(t.data_ptr())
+        self._after_engine()
+        return (t.cpu() if self.host_staging else t), nb
+
+    def merge_runs_tensor(self, t: torch.Tensor, run_bytes: List[int]):
+        if not t.is_cuda:
+            t = t.to("cuda")
+        self._before_engine()
+        return self.e.merge_runs(t.data_ptr(), run_bytes)     # synchronous

@@ -100,8 +100,24 @@ def _listen(addr: str) -> socket.socket:
 
 
 # ---------------------------------------------------------------- Split / Merge (host)
+def _atomic_write(path: str, data: bytes) -> None:
+    """Write a job's output file as temp-then-rename: a worker killed mid-write never leaves a
+    truncated file under the reference's name, and a re-executed job replaces it whole (the
+    reference truncates in place with os.Create, mapreduce.go:215,270)."""
+    tmp = f"{path}.tmp{os.getpid()}.{threading.get_ident()}"
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, path)
+
+
 def split(path: str, nmap: int, workdir: str, fname: str) -> int:
-    """Split (mapreduce.go:141-179); returns the number of split files written."""
+    """Split (mapreduce.go:141-179); returns the number of split files written.
+
+    Quirk P1 is kept: bufio.Scanner's buffer holds at most 64 KiB, so a line that does not fit
+    with its '\n' (65,536 bytes or more before the '\n', or at the end of the input) stops the
+    scan silently, and the rest of the input is never split (the reference checks no scanner
+    error after its loop, mapreduce.go:164-176)."""
+    print(f"Split {fname}", flush=True)
     data = open(path, "rb").read()
     nchunk = len(data) // nmap + 1
     lines = data.split(b"\n")
@@ -109,8 +125,8 @@ def split(path: str, nmap: int, workdir: str, fname: str) -> int:
         lines.pop()                 # the scanner yields no empty token after a final "\n"
     outs, cur, m, i = [], [], 1, 0
     for line in lines:
-        if len(line) > MAX_LINE:
-            raise ValueError("Split: line longer than bufio.Scanner's 64 KiB limit")
+        if len(line) >= MAX_LINE:
+            break                   # ErrTooLong ends Scan(); the loop just stops (P1)
         if i > nchunk * m:
             outs.append(b"".join(cur))
             cur, m = [], m + 1
@@ -120,8 +136,7 @@ def split(path: str, nmap: int, workdir: str, fname: str) -> int:
         i += len(line) + 1
     outs.append(b"".join(cur))
     for k, b in enumerate(outs):
-        with open(os.path.join(workdir, map_name(fname, k)), "wb") as f:
-            f.write(b)
+        _atomic_write(os.path.join(workdir, map_name(fname, k)), b)
     return len(outs)
 
 
@@ -130,6 +145,7 @@ def merge(workdir: str, fname: str, nreduce: int) -> bytes:
     "%s: %s\\n"; writes mrtmp.<f> and returns its bytes."""
     kvs: Dict[bytes, bytes] = {}
     for r in range(nreduce):
+        print(f"Merge: read {merge_name(fname, r)}", flush=True)
         with open(os.path.join(workdir, merge_name(fname, r)), "rb") as f:
             for line in f:
                 try:
@@ -138,37 +154,99 @@ def merge(workdir: str, fname: str, nreduce: int) -> bytes:
                     break           # a decode error ends the file, as the reference's loop does
                 kvs[kv["Key"].encode()] = kv["Value"].encode()
     out = b"".join(k + b": " + kvs[k] + b"\n" for k in sorted(kvs))
-    with open(os.path.join(workdir, "mrtmp." + fname), "wb") as f:
-        f.write(out)
+    _atomic_write(os.path.join(workdir, "mrtmp." + fname), out)
     return out
 
 
 # ---------------------------------------------------------------- GPU DoMap / DoReduce
-def do_map(engine, job: int, workdir: str, fname: str, nreduce: int) -> None:
-    """DoMap (mapreduce.go:193-231) on the GPU: one split -> nReduce record files."""
-    with open(os.path.join(workdir, map_name(fname, job)), "rb") as f:
+EFULL = 4                              # WCG_EFULL (include/wcg.h): aggregation table full
+
+
+def _sized_job(engine, nbytes: int, job):
+    """Run job() on an engine sized for nbytes of input when the engine can be re-sized
+    (wc.SizedEngine.ensure); once more with worst-case tables if its table filled."""
+    ensure = getattr(engine, "ensure", None)
+    if ensure is None:
+        return job()
+    ensure(nbytes)
+    try:
+        return job()
+    except Exception as e:   # WcgError(WCG_EFULL): rerun the whole job with room for every key
+        if getattr(e, "status", None) != EFULL:
+            raise
+    ensure(nbytes, True)
+    return job()
+
+
+def do_map(engine, job: int, workdir: str, fname: str, nreduce: int, json_intermediates: bool = False) -> None:
+    """DoMap (mapreduce.go:193-231) on the GPU: one split -> nReduce intermediate files.
+
+    Default: pre-aggregated 32-byte record units partitioned by ihash % nReduce (what a GPU
+    DoReduce imports).  json_intermediates=True writes the reference's own per-occurrence JSON
+    lines instead ({"Key":"tok","Value":"1"}\n for every token, in input order,
+    mapreduce.go:214-230), byte for byte, so an unmodified CPU DoReduce can consume them."""
+    name = map_name(fname, job)
+    path = os.path.join(workdir, name)
+    print(f"DoMap: read split {name} {os.path.getsize(path)}", flush=True)
+    with open(path, "rb") as f:
         b = f.read()
-    engine.reset()
-    if b:
-        engine.map_host(b)
-    recs, counts = engine.export_host(nreduce, nreduce)
+    if json_intermediates:
+        parts = _sized_job(engine, len(b), lambda: engine.map_json(b, nreduce))
+        for r in range(nreduce):
+            _atomic_write(os.path.join(workdir, reduce_name(fname, job, r)), parts[r])
+        return
+
+    def run():
+        engine.reset()
+        if b:
+            engine.map_host(b)
+        return engine.export_host(nreduce, nreduce)
+    recs, counts = _sized_job(engine, len(b), run)
     off = 0
     for r in range(nreduce):
-        with open(os.path.join(workdir, reduce_name(fname, job, r)), "wb") as f:
-            f.write(recs[off * 32:(off + counts[r]) * 32])
+        _atomic_write(os.path.join(workdir, reduce_name(fname, job, r)), recs[off * 32:(off + counts[r]) * 32])
         off += counts[r]
 
 
 def do_reduce(engine, job: int, workdir: str, fname: str, nmap: int) -> None:
     """DoReduce (mapreduce.go:239-280) on the GPU: partition `job` of every map job -> the
     reference's -res-<job> JSON lines (every imported key belongs to this partition)."""
-    engine.reset()
+    files = []
     for m in range(nmap):
-        with open(os.path.join(workdir, reduce_name(fname, m, job)), "rb") as f:
-            engine.import_host(f.read())
-    engine.reduce()
-    with open(os.path.join(workdir, merge_name(fname, job)), "wb") as f:
-        f.write(engine.partition(1, 0))
+        name = reduce_name(fname, m, job)
+        print(f"DoReduce: read {name}", flush=True)
+        with open(os.path.join(workdir, name), "rb") as f:
+            files.append(f.read())
+    json_in = any(f[:1] == b"{" for f in files)
+
+    def run():
+        engine.reset()
+        for data in files:
+            if json_in:
+                # the reference's -m-r JSON lines (a CPU or json_intermediates DoMap wrote them):
+                # decode on the host as DoReduce's json.Decoder does (mapreduce.go:249-261), one
+                # key per line, and count the keys on the GPU
+                keys = _json_keys(data)
+                if keys:
+                    engine.map_host(keys)
+            else:
+                engine.import_host(data)
+        engine.reduce()
+        return engine.partition(1, 0)
+    # one distinct key per record unit (or per JSON line) at most
+    nunits = sum(len(f) // 32 if not json_in else f.count(b"\n") for f in files)
+    _atomic_write(os.path.join(workdir, merge_name(fname, job)), _sized_job(engine, 16 * nunits, run))
+
+
+def _json_keys(data: bytes) -> bytes:
+    """Keys of {"Key":"k","Value":"1"} lines, newline-separated (the decoder stops at the first
+    line that is not such an object, as the reference's loop ends on a decode error)."""
+    out = []
+    for line in data.split(b"\n"):
+        if not (line.startswith(b'{"Key":"') and line.endswith(b'","Value":"1"}')):
+            break
+        out.append(line[8:-14])
+    return b"\n".join(out) + b"\n" if out else b""
 
 
 # ---------------------------------------------------------------- worker (worker.go)
@@ -177,9 +255,10 @@ class Worker:
     connections (nrpc < 0: unlimited).  Each DoJob runs on this worker's GPU engine."""
 
     def __init__(self, master: str, me: str, engine_factory: Callable[[], object], workdir: str,
-                 nrpc: int = -1):
+                 nrpc: int = -1, json_intermediates: bool = False):
         self.master, self.me, self.workdir = master, me, workdir
         self.nrpc, self.njobs = nrpc, 0
+        self.json_intermediates = json_intermediates
         self.engine = engine_factory()
         self.lock = threading.Lock()            # one job at a time on the engine
         self.l = _listen(me)
@@ -192,9 +271,12 @@ class Worker:
         return self
 
     def DoJob(self, a: dict) -> dict:                       # worker.go:22-34
+        print(f"Dojob {self.me} job {a['JobNumber']} file {a['File']} operation {a['Operation']} "
+              f"N {a['NumOtherPhase']}", flush=True)
         with self.lock:
             if a["Operation"] == MAP:
-                do_map(self.engine, a["JobNumber"], self.workdir, a["File"], a["NumOtherPhase"])
+                do_map(self.engine, a["JobNumber"], self.workdir, a["File"], a["NumOtherPhase"],
+                       self.json_intermediates)
             else:
                 do_reduce(self.engine, a["JobNumber"], self.workdir, a["File"], a["NumOtherPhase"])
         return {"OK": True}
@@ -258,12 +340,15 @@ class MapReduce:
         self.l.close()
         return {}
 
-    def _run(self) -> None:
+    def _run(self) -> None:                                 # mapreduce.go:369-380
         try:
+            print(f"Run mapreduce job {self.addr} {self.file}", flush=True)
             self.nsplits = split(self.path, self.nmap, self.workdir, self.file)
             self.stats = self.run_master()
             self.merged = merge(self.workdir, self.file, self.nreduce)
-            call(self.addr, "MapReduce.Shutdown", {})
+            if call(self.addr, "MapReduce.Shutdown", {}) is None:
+                print(f"Cleanup: RPC {self.addr} error", flush=True)
+            print(f"{self.addr}: MapReduce done", flush=True)
         except BaseException as e:   # reported through wait()
             self.error = e
         finally:
@@ -348,18 +433,21 @@ def run_single(nmap: int, nreduce: int, path: str, engine, workdir: str) -> byte
     """RunSingle with the wc UDFs on one GPU: Split as the reference does, every split mapped
     into one engine, the nReduce -res-<r> files and the merged mrtmp.<f> written from it."""
     fname = os.path.basename(path)
-    n = split(path, nmap, workdir, fname)
+    split(path, nmap, workdir, fname)
     engine.reset()
-    for m in range(n):
-        with open(os.path.join(workdir, map_name(fname, m)), "rb") as f:
+    for m in range(nmap):       # fewer split files than nMap (P3): open fails, as DoMap's does
+        name = map_name(fname, m)
+        print(f"DoMap: read split {name} {os.path.getsize(os.path.join(workdir, name))}", flush=True)
+        with open(os.path.join(workdir, name), "rb") as f:
             b = f.read()
         if b:
             engine.map_host(b)
     engine.reduce()
+    parts = engine.partitions(nreduce)          # every -res-<r> in one formatting pass
     for r in range(nreduce):
-        with open(os.path.join(workdir, merge_name(fname, r)), "wb") as f:
-            f.write(engine.partition(nreduce, r))
+        _atomic_write(os.path.join(workdir, merge_name(fname, r)), parts[r])
     out = engine.result()
-    with open(os.path.join(workdir, "mrtmp." + fname), "wb") as f:
-        f.write(out)
+    for r in range(nreduce):
+        print(f"Merge: read {merge_name(fname, r)}", flush=True)
+    _atomic_write(os.path.join(workdir, "mrtmp." + fname), out)
     return out

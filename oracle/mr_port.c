@@ -21,6 +21,7 @@
  */
 #include <fcntl.h>
 #include <stdint.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -197,6 +198,55 @@ WCO_API int mrp_run_single(const char *dir, const char *file, int nmap, int nred
     if (made != nmap) return -1;
     for (int i = 0; i < nmap; i++) do_map(dir, file, i, nreduce);
     for (int r = 0; r < nreduce; r++) do_reduce(dir, file, r, nmap);
+    merge(dir, file, nreduce);
+    return 0;
+}
+
+/* DoReduce(job) alone (mapreduce.go:239-280): reads mrtmp.<file>-<m>-<job> for m < nmap in dir,
+ * which any DoMap wrote (tests: the GPU's JSON intermediates, wcg_map_json). */
+WCO_API void mrp_do_reduce(const char *dir, const char *file, int job, int nmap) { do_reduce(dir, file, job, nmap); }
+
+/* The distributed master/worker path's work on one host (master.go:29-88, worker.go:22-34):
+ * Split, then nworkers worker threads take map jobs from the master's queue until the map phase
+ * is done (the barrier of master.go:73), then reduce jobs, then Merge.  Same files and formats
+ * as RunSingle; the RPC transport is not modelled (it carries no bytes of the data path). */
+typedef struct {
+    const char *dir, *file;
+    int nmap, nreduce, next_job, phase;
+    pthread_mutex_t mu;
+    pthread_barrier_t bar;
+} par_t;
+
+static void *par_worker(void *arg) {
+    par_t *p = (par_t *)arg;
+    for (int phase = 0; phase < 2; phase++) {
+        while (1) {
+            pthread_mutex_lock(&p->mu);
+            const int j = p->next_job++;
+            pthread_mutex_unlock(&p->mu);
+            if (phase == 0 ? j >= p->nmap : j >= p->nreduce) break;
+            if (phase == 0) do_map(p->dir, p->file, j, p->nreduce);
+            else do_reduce(p->dir, p->file, j, p->nmap);
+        }
+        if (pthread_barrier_wait(&p->bar) == PTHREAD_BARRIER_SERIAL_THREAD) p->next_job = 0;
+        pthread_barrier_wait(&p->bar);
+    }
+    return NULL;
+}
+
+WCO_API int mrp_run_parallel(const char *dir, const char *file, int nmap, int nreduce, int nworkers) {
+    int made = split(dir, file, nmap);
+    if (made != nmap) return -1;
+    par_t p;
+    p.dir = dir; p.file = file; p.nmap = nmap; p.nreduce = nreduce; p.next_job = 0; p.phase = 0;
+    pthread_mutex_init(&p.mu, NULL);
+    pthread_barrier_init(&p.bar, NULL, (unsigned)nworkers);
+    pthread_t *th = (pthread_t *)calloc((size_t)nworkers, sizeof(pthread_t));
+    for (int i = 0; i < nworkers; i++) pthread_create(&th[i], NULL, par_worker, &p);
+    for (int i = 0; i < nworkers; i++) pthread_join(th[i], NULL);
+    pthread_barrier_destroy(&p.bar);
+    pthread_mutex_destroy(&p.mu);
+    free(th);
     merge(dir, file, nreduce);
     return 0;
 }

@@ -9,6 +9,14 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same soname as
+# /opt/rocm's).  Loading torch first makes libwcg bind to the runtime torch uses; loading libwcg
+# first would put the system runtime under torch, which then finds no GPU.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box via gpurun)")

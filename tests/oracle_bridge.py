@@ -45,6 +45,10 @@ def lib() -> ctypes.CDLL:
         L.wco_tokens.argtypes = [ctypes.c_char_p, U64, ctypes.POINTER(U64), ctypes.POINTER(U32), U64]
         L.mrp_run_single.restype = ctypes.c_int
         L.mrp_run_single.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        L.mrp_run_parallel.restype = ctypes.c_int
+        L.mrp_run_parallel.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.mrp_do_reduce.restype = None
+        L.mrp_do_reduce.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -96,3 +100,30 @@ def tokens(data: bytes):
 
 def run_single_files(directory: str, file: str, nmap: int, nreduce: int) -> int:
     return lib().mrp_run_single(directory.encode(), file.encode(), nmap, nreduce)
+
+
+def run_parallel_files(directory: str, file: str, nmap: int, nreduce: int, nworkers: int) -> int:
+    """The master/worker path's work with nworkers worker threads (oracle/mr_port.c)."""
+    return lib().mrp_run_parallel(directory.encode(), file.encode(), nmap, nreduce, nworkers)
+
+
+def do_reduce_files(directory: str, file: str, job: int, nmap: int) -> None:
+    """The CPU DoReduce (mapreduce.go:239-280) over mrtmp.<file>-<m>-<job> files in directory."""
+    lib().mrp_do_reduce(directory.encode(), file.encode(), job, nmap)
+
+
+def first_diff(got: bytes, want: bytes) -> str:
+    """A short description of where two merged files first differ (pytest's own diff of
+    multi-megabyte byte strings takes minutes)."""
+    if got == want:
+        return "equal"
+    g, w = got.splitlines(keepends=True), want.splitlines(keepends=True)
+    for i, (a, b) in enumerate(zip(g, w)):
+        if a != b:
+            return f"line {i}: got {a[:80]!r} want {b[:80]!r} ({len(g)} vs {len(w)} lines)"
+    return f"prefix equal, {len(g)} vs {len(w)} lines, {len(got)} vs {len(want)} bytes"
+
+
+def assert_same(got: bytes, want: bytes) -> None:
+    if got != want:
+        raise AssertionError(first_diff(got, want))

@@ -3,7 +3,8 @@
 The GPU engine cannot run here, so each rank drives the orchestration with an oracle-backed
 stand-in that speaks libwcg's 32-byte record-unit wire format (include/wcg.h, WCG_RECORD_BYTES).
 This checks the range partitioning, the owner rule (ihash % nReduce) % world, the count +
-payload all-to-all-v, the owner-side reduce and the gather/merge on rank 0 against the oracle.
+payload all-to-all-v, the owner-side reduce (each owner's sorted run) and the k-way merge of the
+runs on rank 0 against the oracle.
 """
 import os
 import socket
@@ -80,6 +81,25 @@ class OracleEngine:
     def result(self):
         return wc_ref.merged_output(self.counts)
 
+    def result_tensor(self):
+        out = self.result()
+        return torch.frombuffer(bytearray(out or b"\0"), dtype=torch.uint8), len(out)
+
+    def merge_runs_tensor(self, t, run_bytes):
+        """k-way merge of sorted "key: count" runs (the owners' disjoint outputs) by key bytes."""
+        import heapq
+        raw, runs, off = t.numpy().tobytes(), [], 0
+        for n in run_bytes:
+            runs.append(raw[off:off + n].splitlines(keepends=True))
+            off += n
+        for run in runs:
+            keys = [l.rsplit(b": ", 1)[0] for l in run]
+            assert keys == sorted(keys), "a run is not sorted"
+        merged = list(heapq.merge(*runs, key=lambda l: l.rsplit(b": ", 1)[0]))
+        self.counts = {l.rsplit(b": ", 1)[0]: int(l.rsplit(b": ", 1)[1]) for l in merged}
+        assert b"".join(merged) == self.result()
+        return len(merged), len(self.result())
+
 
 def corpus():
     from wcg.corpus import Generator
@@ -99,7 +119,7 @@ def _worker(rank, world, port, q):
         wd.shuffle_reduce(eng, R)
         owned = set(eng.counts)
         assert all((wc_ref.ihash(k) % R) % world == rank for k in owned)
-        merged = wd.gather_merge(eng, OracleEngine() if rank == 0 else None)
+        merged = wd.gather_merge(eng)
         if rank == 0:
             q.put(("ok", merged == wc_ref.merged_output(wc_ref.word_count(data))))
         dist.barrier()

@@ -40,7 +40,7 @@ def _worker(rank, world, port, q):
         data = _corpus()
         lo, hi = wd.line_aligned_ranges(len(data), world, lambda i: data[i])[rank]
         R = 64
-        with wcg.Engine(0, max(hi - lo, 1), 1 << 19) as eng, wcg.Engine(0, 0, 1 << 19) as root:
+        with wcg.Engine(0, max(hi - lo, 1), 1 << 19) as eng:
             te = wd.TorchEngine(eng, host_staging=True)
             want = ob.merged(data) if rank == 0 else None
             for rep in range(2):
@@ -49,7 +49,7 @@ def _worker(rank, world, port, q):
                 wd.shuffle_reduce(te, R)
                 owned = eng.result().splitlines()
                 owner_ok = all((wcg.ihash(l.rsplit(b": ", 1)[0]) % R) % world == rank for l in owned)
-                merged = wd.gather_merge(te, wd.TorchEngine(root, host_staging=True) if rank == 0 else None)
+                merged = wd.gather_merge(te)          # rank 0 merges the owners' sorted runs
                 q.put((rank, rep, owner_ok, len(owned), merged == want if rank == 0 else None))
         dist.barrier()
         dist.destroy_process_group()

@@ -94,7 +94,7 @@ def test_random_bytes(eng):
         while len(out) < n:
             out += rng.choice(pool) if rng.random() < 0.8 else bytes([rng.randrange(256)])
         d = bytes(out)
-        assert gpu_wc(eng, d) == ob.merged(d)
+        ob.assert_same(gpu_wc(eng, d), ob.merged(d))
 
 
 def test_many_distinct_keys_force_global_path(eng):
@@ -102,7 +102,7 @@ def test_many_distinct_keys_force_global_path(eng):
     keys = [("k%x" % i).translate(str.maketrans("0123456789", "ghijklmnop")).encode() for i in range(300_000)]
     random.Random(3).shuffle(keys)
     d = b" ".join(keys) + b"\n"
-    assert gpu_wc(eng, d) == ob.merged(d)
+    ob.assert_same(gpu_wc(eng, d), ob.merged(d))
     st = eng.stats()
     assert st["global_ops"] > 0
 
@@ -121,7 +121,7 @@ def test_long_keys_and_prefix_ties(eng):
         words.append(p + tail)
     words += [b"q" * rng.randrange(1, 300) for _ in range(500)]
     d = b" ".join(words) + b"\n"
-    assert gpu_wc(eng, d) == ob.merged(d)
+    ob.assert_same(gpu_wc(eng, d), ob.merged(d))
 
 
 def test_long_keys_hot_cached_and_cell_sizes(eng):
@@ -139,8 +139,8 @@ def test_long_keys_hot_cached_and_cell_sizes(eng):
         words.append(rng.choice(hot) if rng.random() < 0.6 else rng.choice(vocab))
     d = b" ".join(words) + b"\n"
     want = ob.merged(d)
-    assert gpu_wc(eng, d) == want
-    assert gpu_wc(eng, d, splits=3) == want
+    ob.assert_same(gpu_wc(eng, d), want)
+    ob.assert_same(gpu_wc(eng, d, splits=3), want)
     st = eng.stats()
     assert st["long_tokens"] == 400_000 and st["overflow"] == 0 and st["spin_fail"] == 0
 
@@ -150,7 +150,7 @@ def test_corpus_multi_split(eng, mode):
     from wcg.corpus import Generator
     d = Generator(mode, 50_000, 1.0, 21).bytes(24 << 20)
     want = ob.merged(d)
-    assert gpu_wc(eng, d) == want
+    ob.assert_same(gpu_wc(eng, d), want)
     assert gpu_wc(eng, d, splits=5) == want        # DoMap per split accumulates (RunSingle M=5)
     st = eng.stats()
     assert st["overflow"] == 0 and st["spin_fail"] == 0
@@ -221,5 +221,5 @@ def test_full_size_c2(built):
         st = e.stats()
     data = host.numpy().tobytes()
     r = ob.Result(data, 16)
-    assert got == r.merged()
+    ob.assert_same(got, r.merged())
     assert st["tokens"] == r.ntokens and nk == r.nkeys

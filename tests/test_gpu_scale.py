@@ -1,0 +1,100 @@
+"""GPU: parity at the configs' scale and over the whole Unicode range, bit-exact.
+
+  * every Unicode scalar value 0x80-0x10FFFF through the kernel's UTF-8 decoder and letter
+    table, one per token and in runs that straddle 16-byte chunks, against the C oracle;
+  * C4's key cardinality: the first GiB of the C4 generator (2.4e7 distinct keys) through
+    several wcg_map_device calls into one context sized for 5e7 keys;
+  * a C3-shaped job: 2 GiB of the C3 generator, nReduce = 64, all 64 -res-<r> files.
+"""
+import pytest
+
+from tests import oracle_bridge as ob
+
+pytestmark = pytest.mark.gpu
+
+
+def _scalars():
+    return [cp for cp in range(0x80, 0x110000) if not (0xD800 <= cp <= 0xDFFF)]
+
+
+@pytest.mark.parametrize("layout", ["separated", "runs"])
+def test_every_unicode_scalar(built, layout):
+    import wcg
+    cps = _scalars()
+    if layout == "separated":
+        data = b" ".join(chr(cp).encode() for cp in cps) + b"\n"
+    else:
+        # runs of 1..7 code points with 0..15 ASCII letters in front, so runs start at every
+        # byte offset of a 16-byte chunk and straddle chunk edges
+        parts, i, k = [], 0, 0
+        while i < len(cps):
+            n = 1 + k % 7
+            parts.append(b"a" * (k % 16) + "".join(chr(c) for c in cps[i:i + n]).encode() + b"\x80" * (k % 2) + b" ")
+            i += n
+            k += 1
+        data = b"".join(parts) + b"\n"
+    with wcg.Engine(0, 0, 1 << 21) as e:
+        e.reset()
+        e.map_host(data)
+        e.reduce()
+        ob.assert_same(e.result(), ob.merged(data))
+
+
+@pytest.fixture(scope="module")
+def c4_gib(built):
+    import torch
+    from wcg.corpus import Generator, CONFIGS
+    cfg = CONFIGS["c4_utf8_zipf_64gib"]
+    n = 1 << 30
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    print("c4: building the 5e7-word generator", flush=True)
+    Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"]).fill_ptr(host.data_ptr(), n)
+    print("c4: 1 GiB generated", flush=True)
+    return host
+
+
+@pytest.mark.timeout(600)
+def test_c4_gib_5e7_key_table_multi_call(c4_gib):
+    import torch
+    import wcg
+    host = c4_gib
+    n = host.numel()
+    data = host.numpy().tobytes()
+    dev = host.to("cuda")
+    torch.cuda.synchronize()
+    q = n // 4                                               # 1 MiB generator blocks end in '\n'
+    with wcg.Engine(0, 0, 50_000_000) as e:
+        e.reset()
+        for k in range(4):                                   # four DoMap calls into one table
+            e.map_device(dev.data_ptr() + k * q, q)
+        nk, nb = e.reduce()
+        got = e.result()
+        st = e.stats()
+    print(f"c4: GPU done, {nk} keys; oracle counting", flush=True)
+    r = ob.Result(data, 16)
+    assert nk == r.nkeys and nk > 20_000_000
+    assert st["tokens"] == r.ntokens and st["overflow"] == 0
+    ob.assert_same(got, r.merged())
+
+
+@pytest.mark.timeout(600)
+def test_c3_shaped_2gib_nreduce_64(built):
+    import torch
+    import wcg
+    from wcg.corpus import Generator, CONFIGS
+    cfg = CONFIGS["c3_ascii_zipf_16gib"]
+    n = 2 << 30
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"]).fill_ptr(host.data_ptr(), n)
+    dev = host.to("cuda")
+    torch.cuda.synchronize()
+    with wcg.Engine(0, 0, 1 << 20) as e:
+        e.reset()
+        e.map_device(dev.data_ptr(), n)
+        e.reduce()
+        parts = e.partitions(64)
+        merged = e.result()
+    del dev
+    r = ob.Result(host.numpy().tobytes(), 16)
+    ob.assert_same(merged, r.merged())
+    assert parts == [r.res(64, i) for i in range(64)]

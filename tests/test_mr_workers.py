@@ -48,6 +48,15 @@ class StandInEngine:
     def partition(self, nreduce, r):
         return wc_ref.res_file(self.counts, nreduce, r)
 
+    def partitions(self, nreduce):
+        return [self.partition(nreduce, r) for r in range(nreduce)]
+
+    def result(self):
+        return wc_ref.merged_output(self.counts)
+
+    def map_json(self, data, nreduce):
+        return wc_ref.map_files(data, nreduce)
+
 
 def _input(tmp_path, nbytes=300_000):
     from wcg.corpus import Generator
@@ -133,6 +142,43 @@ def test_split_matches_reference_rules(tmp_path):
     assert b"".join(parts) == b"ab cd\nef\n\ngh ij kl\nlast\n"
     # size 25, nchunk = 25 // 3 + 1 = 9: a new split starts once more than 9 * m bytes were written
     assert parts == [b"ab cd\nef\n\n", b"gh ij kl\n", b"last\n"]
+
+
+def test_split_p1_line_limit(tmp_path):
+    """Quirk P1 (bufio.Scanner, mapreduce.go:164-176): a line of 65,535 bytes is split like any
+    other; one of 65,536 bytes (with or without its '\n') ends the scan silently - the lines
+    before it are the whole input, as in the oracle's restatement."""
+    from wcg import mr
+    for L, stops in ((65535, False), (65536, True), (70000, True)):
+        for tail in (b"\nafter line\n", b""):
+            data = b"first line\n" + b"y" * L + tail
+            p = tmp_path / f"in{L}{len(tail)}.txt"
+            p.write_bytes(data)
+            n = mr.split(str(p), 1, str(tmp_path), p.name)
+            got = b"".join((tmp_path / mr.map_name(p.name, k)).read_bytes() for k in range(n))
+            assert got == b"".join(wc_ref.split(data, 1)), (L, tail)
+            assert (got == b"first line\n") == stops
+
+
+def test_json_intermediates_cpu_standin(tmp_path):
+    """json_intermediates: DoMap writes the reference's per-occurrence JSON lines and DoReduce
+    reads them back (the file formats and names the CPU DoReduce / CleanupFiles expect)."""
+    from wcg import mr
+    path, data = _input(tmp_path, 100_000)
+    fname = os.path.basename(path)
+    nmap, nreduce = 4, 3
+    n = mr.split(path, nmap, str(tmp_path), fname)
+    eng = StandInEngine()
+    for m in range(n):
+        mr.do_map(eng, m, str(tmp_path), fname, nreduce, json_intermediates=True)
+        split = (tmp_path / mr.map_name(fname, m)).read_bytes()
+        want = wc_ref.map_files(split, nreduce)
+        for r in range(nreduce):
+            assert (tmp_path / mr.reduce_name(fname, m, r)).read_bytes() == want[r]
+    counts = _expected(data)
+    for r in range(nreduce):
+        mr.do_reduce(eng, r, str(tmp_path), fname, n)
+        assert (tmp_path / mr.merge_name(fname, r)).read_bytes() == wc_ref.res_file(counts, nreduce, r)
 
 
 @pytest.mark.gpu
