@@ -235,6 +235,11 @@ int dbg(wcg_ctx* c, const char* what) {
 // exclusive scan of m u32 in place (multi-block)
 int scan_u32(wcg_ctx* c, u32* v, u64 m) {
     const u64 nb = cdiv(m, SC_SEG);
+    if (nb == 1) {                                 // one segment: one workgroup, one launch
+        k_scan_apply1<<<1, SC_NT, 0, c->stream>>>(v, m);
+        HIPCHK(c, hipGetLastError());
+        return WCG_OK;
+    }
     RC(ensure(c, &c->spart, &c->spart_cap, nb + 1));
     k_scan_part<<<(unsigned)nb, SC_NT, 0, c->stream>>>(v, m, c->spart);
     k_scan_u64<<<1, 1024, 0, c->stream>>>(c->spart, nb, nullptr);
@@ -309,22 +314,32 @@ int sort_records(wcg_ctx* c) {
     a.smp = nullptr;
     if (a.B > 1) {
         RC(ensure(c, &c->smp, &c->smp_cap, 2 * a.S));
-        k_ss_sample<<<(unsigned)cdiv(a.S, 256), 256, 0, c->stream>>>(a, c->smp);
+        if (a.S <= TS_TILE) {                      // one workgroup samples and sorts
+            k_ss_sample_sort<<<1, TS_NT, 0, c->stream>>>(a, c->smp);
+            a.smp = c->smp;
+        } else {
+            k_ss_sample<<<(unsigned)cdiv(a.S, 256), 256, 0, c->stream>>>(a, c->smp);
+            Rec* s = nullptr;
+            RC(merge_sort(c, c->smp, c->smp + a.S, a.S, &s));
+            a.smp = s;
+        }
         HIPCHK(c, hipGetLastError());
-        Rec* s = nullptr;
-        RC(merge_sort(c, c->smp, c->smp + a.S, a.S, &s));
-        a.smp = s;
     }
-    a.G = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, 4096), (u64)c->ncu));
+    const bool small = a.B <= SS_LDSB;
+    // enough workgroups that each thread takes a few records (the bucket search is a chain of
+    // dependent reads); the large-B kernels keep one 128 KiB histogram per CU
+    a.G = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, small ? 1024 : 4096), (u64)c->ncu * (small ? 4 : 1)));
     RC(ensure(c, &c->bid, &c->bid_cap, n));
     RC(ensure(c, &c->hist, &c->hist_cap, (u64)a.B * a.G));
     RC(ensure_items(c, 2 * n));
     a.bid = c->bid; a.hist = c->hist;
     a.ikey = c->ikey; a.iidx = c->iidx; a.ikey2 = c->ikey + n; a.iidx2 = c->iidx + n;
-    k_ss_hist<<<a.G, SS_NT, 0, c->stream>>>(a);
+    if (small) k_ss_hist<true><<<a.G, SS_NT, 0, c->stream>>>(a);
+    else k_ss_hist<false><<<a.G, SS_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
     RC(scan_u32(c, c->hist, (u64)a.B * a.G));
-    k_ss_scatter<<<a.G, SS_NT, 0, c->stream>>>(a);
+    if (small) k_ss_scatter<true><<<a.G, SS_NT, 0, c->stream>>>(a);
+    else k_ss_scatter<false><<<a.G, SS_NT, 0, c->stream>>>(a);
     k_ss_bucket<<<a.B, SB_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
     if (c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA));

@@ -258,6 +258,29 @@ __global__ __launch_bounds__(SC_NT) void k_scan_apply(u32* v, u64 n, const u64* 
     }
 }
 
+// a single segment (m <= SC_SEG): exclusive scan from 0
+__global__ __launch_bounds__(SC_NT) void k_scan_apply1(u32* v, u64 m) {
+    __shared__ u64 ws[SC_NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u64 base = (u64)tid * SC_IPT;
+    u32 x[SC_IPT];
+    u64 s = 0;
+#pragma unroll
+    for (int k = 0; k < SC_IPT; k++) { x[k] = base + k < m ? v[base + k] : 0u; s += x[k]; }
+    u64 incl = s;
+    for (int d = 1; d < 64; d <<= 1) { const u64 y = __shfl_up(incl, d, 64); if (lane >= d) incl += y; }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    u64 pre = 0;
+    for (int k = 0; k < w; k++) pre += ws[k];
+    u64 run = pre + incl - s;
+#pragma unroll
+    for (int k = 0; k < SC_IPT; k++) {
+        if (base + k < m) v[base + k] = (u32)run;
+        run += x[k];
+    }
+}
+
 // ---------------------------------------------------------------- sample sort
 constexpr u32 SS_TARGET = 2048;        // expected records per bucket
 constexpr u32 SS_CAP = 4096;           // bucket size sorted in LDS (larger: the global path)
@@ -310,15 +333,38 @@ __device__ __forceinline__ void ss_range(const SortArgs& a, u64& i0, u64& i1) {
     i1 = a.n * (blockIdx.x + 1) / a.G;
 }
 
+// Up to SS_LDSB buckets the splitters are staged in LDS (a binary search of LDS reads instead of
+// dependent global loads), and the histogram is small: several workgroups fit a CU.
+constexpr u32 SS_LDSB = 2048;
+
+template <bool SMALL>
 __global__ __launch_bounds__(SS_NT) void k_ss_hist(SortArgs a) {
-    __shared__ u32 h[SS_MAXB];
-    for (u32 b = threadIdx.x; b < a.B; b += SS_NT) h[b] = 0;
+    __shared__ u32 h[SMALL ? SS_LDSB : SS_MAXB];
+    __shared__ u64 sp_hi[SMALL ? SS_LDSB : 1], sp_lo[SMALL ? SS_LDSB : 1];
+    __shared__ u32 sp_i[SMALL ? SS_LDSB : 1];
+    for (u32 b = threadIdx.x; b < a.B; b += SS_NT) {
+        h[b] = 0;
+        if (SMALL && b + 1 < a.B) {
+            const Rec& s = a.smp[(u64)(b + 1) * a.S / a.B];
+            sp_hi[b] = s.hi; sp_lo[b] = s.lo; sp_i[b] = (u32)s.cnt;
+        }
+    }
     __syncthreads();
     u64 i0, i1;
     ss_range(a, i0, i1);
     for (u64 i = i0 + threadIdx.x; i < i1; i += SS_NT) {
         const Rec r = a.rec[i];
-        const u32 b = ss_bucket(a, r.hi, r.lo, (u32)i);
+        u32 b;
+        if (SMALL) {
+            u32 l = 0, hh = a.B - 1;
+            while (l < hh) {
+                const u32 mid = (l + hh) >> 1;
+                if (!key3_lt(r.hi, r.lo, (u32)i, sp_hi[mid], sp_lo[mid], sp_i[mid])) l = mid + 1; else hh = mid;
+            }
+            b = l;
+        } else {
+            b = ss_bucket(a, r.hi, r.lo, (u32)i);
+        }
         a.bid[i] = b;
         atomicAdd(&h[b], 1u);
     }
@@ -326,10 +372,47 @@ __global__ __launch_bounds__(SS_NT) void k_ss_hist(SortArgs a) {
     for (u32 b = threadIdx.x; b < a.B; b += SS_NT) a.hist[(u64)b * a.G + blockIdx.x] = h[b];
 }
 
+// the sample of a small sort (S <= TS_TILE): gathered and sorted in one workgroup's LDS,
+// stable (ties by sample position = record order)
+__global__ __launch_bounds__(TS_NT) void k_ss_sample_sort(SortArgs a, Rec* smp) {
+    __shared__ u64 sh[TS_TILE], sl[TS_TILE];
+    __shared__ uint16_t si[TS_TILE];
+    const int tid = threadIdx.x;
+    u32 P = 2;
+    while (P < a.S) P <<= 1;
+    for (u32 j = tid; j < P; j += TS_NT) {
+        if (j < a.S) {
+            const Rec r = a.rec[j * a.n / a.S];
+            sh[j] = r.hi; sl[j] = r.lo;
+        } else { sh[j] = ~0ull; sl[j] = ~0ull; }
+        si[j] = (uint16_t)j;
+    }
+    __syncthreads();
+    for (u32 k = 2; k <= P; k <<= 1)
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+            for (u32 t = tid; t < P / 2; t += TS_NT) {
+                const u32 i = 2 * t - (t & (j - 1)), p = i + j;
+                const u64 ah = sh[i], al = sl[i], bh = sh[p], bl = sl[p];
+                const uint16_t ai = si[i], bi = si[p];
+                if (key3_lt(bh, bl, bi, ah, al, ai) == ((i & k) == 0)) {
+                    sh[i] = bh; sl[i] = bl; sh[p] = ah; sl[p] = al;
+                    si[i] = bi; si[p] = ai;
+                }
+            }
+            __syncthreads();
+        }
+    for (u32 j = tid; j < a.S; j += TS_NT) {
+        Rec s;
+        s.hi = sh[j]; s.lo = sl[j]; s.cnt = (u64)si[j] * a.n / a.S; s.ref = 0;
+        smp[j] = s;
+    }
+}
+
 // items of workgroup g go to [hist[b][g], ...) of their bucket; the order inside a bucket does
 // not matter (the bucket sort orders by (hi, lo, index) completely)
+template <bool SMALL>
 __global__ __launch_bounds__(SS_NT) void k_ss_scatter(SortArgs a) {
-    __shared__ u32 cur[SS_MAXB];
+    __shared__ u32 cur[SMALL ? SS_LDSB : SS_MAXB];
     for (u32 b = threadIdx.x; b < a.B; b += SS_NT) cur[b] = a.hist[(u64)b * a.G + blockIdx.x];
     __syncthreads();
     u64 i0, i1;

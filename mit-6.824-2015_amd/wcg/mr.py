@@ -104,7 +104,8 @@ def _atomic_write(path: str, data: bytes) -> None:
     """Write a job's output file as temp-then-rename: a worker killed mid-write never leaves a
     truncated file under the reference's name, and a re-executed job replaces it whole (the
     reference truncates in place with os.Create, mapreduce.go:215,270)."""
-    tmp = f"{path}.tmp{os.getpid()}.{threading.get_ident()}"
+    d, base = os.path.split(path)          # a dot name: never taken for a reference file
+    tmp = os.path.join(d, f".{base}.tmp{os.getpid()}.{threading.get_ident()}")
     with open(tmp, "wb") as f:
         f.write(data)
     os.replace(tmp, path)
