@@ -15,6 +15,9 @@
 // so no lane ever waits for another lane's publish.
 #pragma once
 #include "wcg_common.h"
+#ifndef WCG_DIAG_SLOTS
+#define WCG_DIAG_SLOTS 0
+#endif
 
 namespace wcg {
 
@@ -136,8 +139,12 @@ struct MapTable {
     // slot choices from 16-bit fields of h by full-rate 24-bit multiplies (bits 16-31 and
     // 6-21; bits 0-5 are the miss bucket, so a bucket's keys still spread over both choices)
     __device__ __forceinline__ static void slots(u32 h, u32 n, u32& s1, u32& s2) {
+#if WCG_DIAG_SLOTS                           // diagnostics only: conflict-free probes, wrong counts
+        s1 = __lane_id(); s2 = __lane_id() + 64; (void)h; (void)n;
+#else
         s1 = __umul24(h >> 16, n) >> 16;
         s2 = __umul24((h >> 6) & 0xFFFFu, n) >> 16;
+#endif
     }
     // A probe split in two so that k_map can issue its reads together with the next token's:
     // probe() computes the candidate slots and reads them, finish() counts one occurrence of
@@ -158,6 +165,29 @@ struct MapTable {
         p.y1 = *K1a; p.y2 = *K1b;
         return p;
     }
+    // short keys only (k_map's short-entry iterations: every lane holds a valid short key)
+    struct ProbeS { u32 s1, s2; u64 x1, x2; };
+    __device__ __forceinline__ ProbeS probe_short(u32 h) const {
+        ProbeS p;
+        slots(h, (u32)NS, p.s1, p.s2);
+        p.x1 = sk0[p.s1]; p.x2 = sk0[p.s2];
+        return p;
+    }
+    __device__ __forceinline__ bool finish_short(u64 a0, const ProbeS& p) {
+        const bool h1 = p.x1 == a0, hit = h1 || p.x2 == a0;
+        atomicAdd(&scnt[h1 ? p.s1 : p.s2], hit ? 1u : 0u);
+        if (hit || (p.x1 != 0 && p.x2 != 0)) return hit;
+        if (p.x1 == 0) {
+            const u64 old = atomicCAS(&sk0[p.s1], 0ull, a0);
+            if (old == 0 || old == a0) { atomicAdd(&scnt[p.s1], 1u); return true; }
+        }
+        if (p.x2 == 0) {
+            const u64 old = atomicCAS(&sk0[p.s2], 0ull, a0);
+            if (old == 0 || old == a0) { atomicAdd(&scnt[p.s2], 1u); return true; }
+        }
+        return false;
+    }
+
     __device__ __forceinline__ bool finish(bool valid, bool med, u64 a0, u64 a1, const Probe& p) {
         u64* K0 = med ? mk0 : sk0;
         u32* C = med ? mcnt : scnt;

@@ -52,6 +52,15 @@ constexpr int MAP_NM = 1024;                 // LDS medium-key slots (20 B each)
 #define WCG_MAP_SETS 4
 #endif
 constexpr int MAP_SETS = WCG_MAP_SETS;       // steps in flight per wave (2 or 4)
+#ifndef WCG_MASKED_RESERVE
+#define WCG_MASKED_RESERVE 0                 // 1: miss reservations by the missing lanes only
+#endif
+#ifndef WCG_NOWAIT
+#define WCG_NOWAIT 0                         // diagnostics: 1 = never wait for the window loads
+#endif
+#ifndef WCG_PIPE
+#define WCG_PIPE 1                           // token-loop pipeline depth (1 or 2)
+#endif
 constexpr int MAX_MISS_BUCKETS = 256;
 constexpr u32 SST_LEN_SHIFT = 10;            // start entry = window offset | min(run, 16) << 10
 
@@ -498,21 +507,34 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         const bool owner = lane >= 1 && lane <= MAP_OWN;
         u32 starts = owner ? (m & ~((m << 1) | (prevm >> 15)) & 0xFFFFu) : 0u;
         const u32 w32 = m | (nextm << 16);
-        const u32 cnt = __popc(starts);
-        u32 o = 0, total = 0;
+        // Start list, short keys (<= 7 bytes: 89% of C2 tokens) first, then the others: a start
+        // whose letter run reaches 8 bytes has bits b..b+7 of w32 set.  Iterations over short
+        // entries only run a short-key body (one key word, one table, no k1 reads).
+        u32 r8 = w32 & (w32 >> 1);
+        r8 &= r8 >> 2;
+        r8 &= r8 >> 4;
+        const u32 cs = __popc(starts & ~r8), co = __popc(starts & r8);
+        u32 o_s = 0, o_o = 0, tot_s = 0, tot_o = 0;
 #pragma unroll
         for (int b = 0; b < 4; b++) {
-            const u64 bal = __ballot((cnt >> b) & 1);
-            o += __builtin_amdgcn_mbcnt_hi((u32)(bal >> 32), __builtin_amdgcn_mbcnt_lo((u32)bal, 0u)) << b;
-            total += (u32)__popcll(bal) << b;
+            const u64 bs = __ballot((cs >> b) & 1), bo = __ballot((co >> b) & 1);
+            o_s += __builtin_amdgcn_mbcnt_hi((u32)(bs >> 32), __builtin_amdgcn_mbcnt_lo((u32)bs, 0u)) << b;
+            o_o += __builtin_amdgcn_mbcnt_hi((u32)(bo >> 32), __builtin_amdgcn_mbcnt_lo((u32)bo, 0u)) << b;
+            tot_s += (u32)__popcll(bs) << b;
+            tot_o += (u32)__popcll(bo) << b;
         }
-        total = __builtin_amdgcn_readfirstlane(total);
+        tot_s = __builtin_amdgcn_readfirstlane(tot_s);
+        const u32 total = tot_s + __builtin_amdgcn_readfirstlane(tot_o);
+        o_o += tot_s;
         while (starts) {
             const u32 b = __builtin_ctz(starts);
             starts &= starts - 1;
             const u32 run = __builtin_ctz(~(w32 >> b));        // >= 1; 32 - b when the window is all letters
             const u32 len = run < 16 ? run : 16u;              // 16 = long token (> 15 bytes)
-            sst[o++] = (uint16_t)((16 * lane + b) | (len << SST_LEN_SHIFT));
+            const bool sh = len < 8;
+            sst[sh ? o_s : o_o] = (uint16_t)((16 * lane + b) | (len << SST_LEN_SHIFT));
+            o_s += sh ? 1u : 0u;
+            o_o += sh ? 0u : 1u;
         }
         wave_lds_sync();
         my_tokens += total;
@@ -525,9 +547,6 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         //      the reservation adds no round trip of its own), and the wave stores the units
         //      then: 2 unit stores per iteration + 2 after the loop (prefetch accounting)
         u32 sink = 0;
-        const u32 iters = (total + 63) >> 6;
-        Tok cur = decode_tok(sst[lane], lane < total, keyread(sst[lane]));
-        u32 e_nxt = sst[64 + lane];
         bool missp = false;                   // the previous iteration's miss: bucket, units,
         u32 pp = 0, nup = 0, posp = 0;        // reservation and key
         u64 k0p = 0, k1p = 0;
@@ -545,8 +564,69 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
                 ginsert(a.gtab, a.gmask, k0p, k1p, gslot(key_hash(k0p, k1p)), 1, a.st);
             }
         };
+        // full iterations of short entries take the short body; the rest (the partial short
+        // iteration, medium and long keys) the general one
+        const u32 nsh = (ABL == 0 || ABL >= 6) ? (tot_s >> 6) : 0u;
+        const u32 first = nsh * 64;
+        const u32 iters = (total - first + 63) >> 6;
+        // one software pipeline over both loops: the short loop's last iteration reads and decodes
+        // the general loop's first token, and neither loop decodes past its last iteration
+        Tok cur;
+        u32 e_nxt;
+        if (nsh) {
+            // short key (<= 7 bytes): its bytes lie in [rp & ~7, +16): two aligned 8-byte reads
+            auto keyread_s = [&](u32 e) -> uint4 {
+                const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1);
+                const uint2* q = reinterpret_cast<const uint2*>(bytes + (rp & ~7u));
+                const uint2 x = q[0], y = q[1];
+                return make_uint4(x.x, x.y, y.x, y.y);
+            };
+            struct TokS { u64 k; u32 h; };
+            auto decode_s = [&](u32 e, const uint4& kw) -> TokS {
+                const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1), len = e >> SST_LEN_SHIFT;
+                const u32 bsh = rp & 3u;
+                const bool hi4 = (rp & 4u) != 0;
+                const u32 e0 = hi4 ? kw.y : kw.x, e1 = hi4 ? kw.z : kw.y, e2 = hi4 ? kw.w : kw.z;
+                const u64 w = (u64)__builtin_amdgcn_alignbyte(e2, e1, bsh) << 32 | __builtin_amdgcn_alignbyte(e1, e0, bsh);
+                TokS t;
+                t.k = (w & ((1ull << (8 * len)) - 1)) | (u64)len << 56;
+                t.h = lds_hash32((u32)t.k, (u32)(t.k >> 32), 0u, 0u);
+                return t;
+            };
+            TokS cs = decode_s(sst[lane], keyread_s(sst[lane]));
+            e_nxt = sst[64 + lane];
+            for (u32 it = 0; it < nsh; it++) {
+                const bool more = it + 1 < nsh;                        // wave-uniform
+                const auto pr = tab.probe_short(cs.h);
+                uint4 nks;
+                KeyWords nkg;
+                if (more) nks = keyread_s(e_nxt);
+                else if (iters) nkg = keyread(e_nxt);                 // the general loop's first token
+                const u32 e_nn = sst[(it + 2) * 64 + lane];
+                const bool hit = tab.finish_short(cs.k, pr);
+                my_hits += (u32)hit;
+                store_pending();
+                missp = !hit;
+                pp = miss_bucket(cs.h, a.pmask);
+                nup = 1u;
+#if WCG_MASKED_RESERVE
+                if (missp) posp = atomicAdd(&cursor[pp], 1u);   // only missing lanes touch the cursors
+#else
+                posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
+#endif
+                k0p = cs.k; k1p = 0;
+                if (more) cs = decode_s(e_nxt, nks);
+                else if (iters) cur = decode_tok(e_nxt, first + lane < total, nkg);
+                e_nxt = e_nn;
+            }
+        } else {
+            cur = decode_tok(sst[lane], lane < total, keyread(sst[lane]));
+            e_nxt = sst[64 + lane];
+        }
         for (u32 it = 0; it < iters; it++) {
-            if (ABL == 1) { sink += cur.e; cur.e = sst[(it + 1) * 64 + lane]; continue; }
+            const u32 base = first + it * 64;
+            const bool more = it + 1 < iters;                          // wave-uniform
+            if (ABL == 1) { sink += cur.e; cur.e = sst[base + 64 + lane]; continue; }
             if (cur.lng) {
                 my_long++;
                 const u32 rp = cur.e & ((1u << SST_LEN_SHIFT) - 1);
@@ -554,29 +634,34 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             }
             const bool med = !cur.shrt;
             const u64 k0 = (u64)cur.k0h << 32 | cur.k0l, k1 = (u64)cur.k1h << 32 | cur.k1l;
-            if (ABL == 2) { sink += cur.h; cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, keyread(e_nxt));
-                            e_nxt = sst[(it + 2) * 64 + lane]; continue; }
+            if (ABL == 2) { sink += cur.h; cur = decode_tok(e_nxt, base + 64 + lane < total, keyread(e_nxt));
+                            e_nxt = sst[base + 128 + lane]; continue; }
             // issue together: this token's probe, the next token's key bytes, the entry after
             const auto pr = tab.probe(med, cur.h);
-            const KeyWords nkw = keyread(e_nxt);
-            const u32 e_nn = sst[(it + 2) * 64 + lane];
+            KeyWords nkw;
+            if (more) nkw = keyread(e_nxt);
+            const u32 e_nn = sst[base + 128 + lane];
             const bool hit = tab.finish(cur.valid, med, k0, k1, pr);
-            if (ABL == 3) { sink += hit; cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, nkw); e_nxt = e_nn; continue; }
+            if (ABL == 3) { sink += hit; if (more) cur = decode_tok(e_nxt, base + 64 + lane < total, nkw); e_nxt = e_nn; continue; }
             my_hits += (u32)hit;
             store_pending();                  // the previous iteration's miss units
             // this token's miss: reserve units in the (workgroup, bucket) region
             missp = cur.valid && !hit;
             pp = miss_bucket(cur.h, a.pmask);
             nup = cur.shrt ? 1u : 2u;
+#if WCG_MASKED_RESERVE
+            if (missp) posp = atomicAdd(&cursor[pp], nup);
+#else
             posp = atomicAdd(&cursor[pp], missp ? nup : 0u);   // every lane (0 = no miss)
+#endif
             k0p = k0; k1p = k1;
-            cur = decode_tok(e_nxt, (it + 1) * 64 + lane < total, nkw);
+            if (more) cur = decode_tok(e_nxt, base + 64 + lane < total, nkw);
             e_nxt = e_nn;
         }
         if (ABL == 0 || ABL >= 6) store_pending();
         if (ABL) asm volatile("" ::"v"(sink));
         wave_lds_sync();
-        return (ABL == 0 || ABL >= 6) ? iters + 1 : 0u;
+        return (ABL == 0 || ABL >= 6) ? nsh + iters + 1 : 0u;
     };
 
     // ---- main loop, unrolled over the register sets so that each set's load and waits name
@@ -601,7 +686,8 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         if (st >= nsteps || is_tail(st)) break;                                                 \
         v4i r; u32 om;                                                                          \
         addr(st + MAP_SETS * stride, r, om);                                                    \
-        set_wait_##S((MAP_SETS - 1) + 2 * (h1 + (MAP_SETS == 4 ? h2 + h3 : 0)), m##S);          \
+        if (WCG_NOWAIT) set_wait_##S(63, m##S); /* diagnostics only: results are wrong */       \
+        else set_wait_##S((MAP_SETS - 1) + 2 * (h1 + (MAP_SETS == 4 ? h2 + h3 : 0)), m##S);     \
         const u32 it_ = process(st, u4(m##S));                                                  \
         set_load_##S(r, om, m##S);                                                              \
         h3 = h2; h2 = h1; h1 = it_;                                                             \

@@ -12,5 +12,5 @@ passes=(
 i=0
 for p in "${passes[@]}"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $p --kernel-include-regex "$KRE" --output-format csv -d "$OUT/pass$i" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify "$@" || exit $?
+  timeout -s KILL 90 rocprofv3 --pmc $p --kernel-include-regex "$KRE" --output-format csv -d "$OUT/pass$i" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-end-to-end "$@" || exit $?
 done
