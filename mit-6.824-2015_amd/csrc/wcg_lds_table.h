@@ -130,11 +130,25 @@ struct MapTable {
     u64* mk1;      // [NM]
     u32* mcnt;     // [NM]
     u64* zero;     // one word, always 0
+    u32* seen;     // admission filter (WCG_ADMIT2): ADMIT_BITS bits, or null
 
     __device__ __forceinline__ void init(int tid, int nt) {
         for (int i = tid; i < NS; i += nt) { sk0[i] = 0; scnt[i] = 0; }
         for (int i = tid; i < NM; i += nt) { mk0[i] = 0; mk1[i] = 0; mcnt[i] = 0; }
+        if (seen) for (int i = tid; i < (int)(ADMIT_BITS / 32); i += nt) seen[i] = 0;
         if (tid == 0) *zero = 0;
+    }
+    // Admission on second sight: a key takes a free slot only if its filter bit was already set
+    // (it missed once before); its first occurrence goes to the miss log like any miss.  The
+    // table then fills with keys that recur, close to the most frequent ones, instead of with the
+    // first distinct keys a workgroup meets (a rare key that shows up early holds its slot for
+    // the whole launch).  Only the insert path, which runs while the table has free slots, pays.
+    static constexpr u32 ADMIT_BITS = 16384;
+    __device__ __forceinline__ bool admit(u32 h) {
+        if (!seen) return true;
+        const u32 b = (h * 0x9E3779B1u) >> 18;
+        const u32 bit = 1u << (b & 31);
+        return (atomicOr(&seen[b >> 5], bit) & bit) != 0;
     }
     // slot choices from 16-bit fields of h by full-rate 24-bit multiplies (bits 16-31 and
     // 6-21; bits 0-5 are the miss bucket, so a bucket's keys still spread over both choices)
@@ -173,10 +187,10 @@ struct MapTable {
         p.x1 = sk0[p.s1]; p.x2 = sk0[p.s2];
         return p;
     }
-    __device__ __forceinline__ bool finish_short(u64 a0, const ProbeS& p) {
+    __device__ __forceinline__ bool finish_short(u64 a0, u32 h, const ProbeS& p) {
         const bool h1 = p.x1 == a0, hit = h1 || p.x2 == a0;
         atomicAdd(&scnt[h1 ? p.s1 : p.s2], hit ? 1u : 0u);
-        if (hit || (p.x1 != 0 && p.x2 != 0)) return hit;
+        if (hit || (p.x1 != 0 && p.x2 != 0) || !admit(h)) return hit;
         if (p.x1 == 0) {
             const u64 old = atomicCAS(&sk0[p.s1], 0ull, a0);
             if (old == 0 || old == a0) { atomicAdd(&scnt[p.s1], 1u); return true; }
@@ -188,13 +202,13 @@ struct MapTable {
         return false;
     }
 
-    __device__ __forceinline__ bool finish(bool valid, bool med, u64 a0, u64 a1, const Probe& p) {
+    __device__ __forceinline__ bool finish(bool valid, bool med, u64 a0, u64 a1, u32 h, const Probe& p) {
         u64* K0 = med ? mk0 : sk0;
         u32* C = med ? mcnt : scnt;
         const bool h1 = p.x1 == a0 && p.y1 == a1, h2 = p.x2 == a0 && p.y2 == a1;
         const bool hit = valid && (h1 || h2);
         atomicAdd(&C[h1 ? p.s1 : p.s2], hit ? 1u : 0u);     // every lane (0 = no hit): no branch
-        if (!valid || hit || (p.x1 != 0 && p.x2 != 0)) return hit;
+        if (!valid || hit || (p.x1 != 0 && p.x2 != 0) || !admit(h)) return hit;
         // insert: claim an empty slot's k0, then publish k1 (a reader that sees k0 before k1
         // treats the slot as another key and may insert a duplicate: harmless, both counts are
         // flushed and summed downstream)

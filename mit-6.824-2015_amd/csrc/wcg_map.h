@@ -46,7 +46,11 @@ constexpr int MAP_STEP = 16 * MAP_OWN;       // 992 input bytes per wave step
 constexpr int MAP_WIN = 1024;                // bytes loaded per step: [step base - 16, + 1024)
 constexpr int MAP_WREG = MAP_WIN + 8;        // staging (+8: keyread's third word at the end)
 constexpr int MAP_SST = 512;                 // max token starts per step (992 / 2 = 496)
-constexpr int MAP_NS = 8896;                 // LDS short-key slots (12 B each)
+#ifndef WCG_ADMIT2
+#define WCG_ADMIT2 1                         // k_map LDS tables admit keys on their second miss
+#endif
+constexpr int MAP_NS = WCG_ADMIT2 ? 8704 : 8896;   // LDS short-key slots (12 B each; the 2 KiB
+                                                  // admission filter takes 192 of them)
 constexpr int MAP_NM = 1024;                 // LDS medium-key slots (20 B each)
 #ifndef WCG_MAP_SETS
 #define WCG_MAP_SETS 4
@@ -402,6 +406,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     __shared__ __align__(16) u64 mk0[MAP_NM];
     __shared__ __align__(16) u64 mk1[MAP_NM];
     __shared__ u64 zero_w;
+    __shared__ u32 seen_w[WCG_ADMIT2 ? MapTable<MAP_NS, MAP_NM>::ADMIT_BITS / 32 : 1];
     __shared__ u32 scnt[MAP_NS];
     __shared__ u32 mcnt[MAP_NM];
     __shared__ u32 cursor[MAX_MISS_BUCKETS];
@@ -409,7 +414,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);     // wave-uniform (scalar)
-    MapTable<MAP_NS, MAP_NM> tab{sk0, scnt, mk0, mk1, mcnt, &zero_w};
+    MapTable<MAP_NS, MAP_NM> tab{sk0, scnt, mk0, mk1, mcnt, &zero_w, WCG_ADMIT2 ? seen_w : nullptr};
     tab.init(tid, MAP_NT);
     for (int i = tid; i < MAX_MISS_BUCKETS; i += MAP_NT) cursor[i] = 0;
     if (tid == 0) lcur = 0;
@@ -603,7 +608,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
                 if (more) nks = keyread_s(e_nxt);
                 else if (iters) nkg = keyread(e_nxt);                 // the general loop's first token
                 const u32 e_nn = sst[(it + 2) * 64 + lane];
-                const bool hit = tab.finish_short(cs.k, pr);
+                const bool hit = tab.finish_short(cs.k, cs.h, pr);
                 my_hits += (u32)hit;
                 store_pending();
                 missp = !hit;
@@ -641,7 +646,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             KeyWords nkw;
             if (more) nkw = keyread(e_nxt);
             const u32 e_nn = sst[base + 128 + lane];
-            const bool hit = tab.finish(cur.valid, med, k0, k1, pr);
+            const bool hit = tab.finish(cur.valid, med, k0, k1, cur.h, pr);
             if (ABL == 3) { sink += hit; if (more) cur = decode_tok(e_nxt, base + 64 + lane < total, nkw); e_nxt = e_nn; continue; }
             my_hits += (u32)hit;
             store_pending();                  // the previous iteration's miss units

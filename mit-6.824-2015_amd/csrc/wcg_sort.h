@@ -282,12 +282,22 @@ __global__ __launch_bounds__(SC_NT) void k_scan_apply1(u32* v, u64 m) {
 }
 
 // ---------------------------------------------------------------- sample sort
-constexpr u32 SS_TARGET = 2048;        // expected records per bucket
+#ifndef WCG_SS_TARGET
+#define WCG_SS_TARGET 512
+#endif
+#ifndef WCG_SS_OVS
+#define WCG_SS_OVS 8
+#endif
+#ifndef WCG_SB_NT
+#define WCG_SB_NT 256
+#endif
+constexpr u32 SS_TARGET = WCG_SS_TARGET;  // expected records per bucket (small buckets: many
+                                          // workgroups sort at once, each bitonic network short)
 constexpr u32 SS_CAP = 4096;           // bucket size sorted in LDS (larger: the global path)
-constexpr u32 SS_OVS = 16;             // samples per bucket
+constexpr u32 SS_OVS = WCG_SS_OVS;     // samples per bucket
 constexpr u32 SS_MAXB = 32768;         // buckets (k_ss_hist / k_ss_scatter LDS: 4 B each)
 constexpr int SS_NT = 256;             // hist / scatter workgroups
-constexpr int SB_NT = 1024;            // bucket sort workgroups
+constexpr int SB_NT = WCG_SB_NT;       // bucket sort workgroups
 
 struct SortArgs {
     const Rec* rec;          // compacted records (index = position)
