@@ -50,6 +50,9 @@ struct wcg_ctx {
     // sort (wcg_sort.h)
     Rec* smp = nullptr; u64 smp_cap = 0;      // 2 x sample records (merge ping-pong)
     u32* bid = nullptr; u64 bid_cap = 0;
+    Rec* irec = nullptr; u64 irec_cap = 0;
+    LEnt* lent = nullptr; u64 lent_cap = 0;   // long-key partitions: LQ x lpart_cap entries
+    u32* lpcur = nullptr; u64 lpcur_cap = 0;    // 2n records: by bucket, and the oversized-bucket scratch
     u32* hist = nullptr; u64 hist_cap = 0;    // [B][G] bucket counts / partition counts
     u64* spart = nullptr; u64 spart_cap = 0;  // multi-block scan partials
     uint4* ikey = nullptr; u32* iidx = nullptr; u64 item_cap = 0;   // 2n items
@@ -302,7 +305,7 @@ int sort_records(wcg_ctx* c) {
         return WCG_OK;
     }
     if (n >= (1ull << 32)) { c->err = "sort: more than 2^32 distinct keys"; return WCG_EINVAL; }
-    // WCG_SORT_TARGET (tests only): records per bucket; above SS_CAP it forces the global path
+    // WCG_SORT_TARGET (tests only): records per bucket; above SB_CAP it forces the global path
     const char* tenv = getenv("WCG_SORT_TARGET");
     const u64 target_env = tenv ? strtoull(tenv, nullptr, 10) : 0;
     u64 target = target_env ? target_env : SS_TARGET;
@@ -331,15 +334,15 @@ int sort_records(wcg_ctx* c) {
     a.G = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, small ? 1024 : 4096), (u64)c->ncu * (small ? 4 : 1)));
     RC(ensure(c, &c->bid, &c->bid_cap, n));
     RC(ensure(c, &c->hist, &c->hist_cap, (u64)a.B * a.G));
-    RC(ensure_items(c, 2 * n));
+    RC(ensure(c, &c->irec, &c->irec_cap, 2 * n));
     a.bid = c->bid; a.hist = c->hist;
-    a.ikey = c->ikey; a.iidx = c->iidx; a.ikey2 = c->ikey + n; a.iidx2 = c->iidx + n;
+    a.irec = c->irec; a.irec2 = c->irec + n;
     if (small) k_ss_hist<true><<<a.G, SS_NT, 0, c->stream>>>(a);
-    else k_ss_hist<false><<<a.G, SS_NT, 0, c->stream>>>(a);
+    else k_ss_hist<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
     RC(scan_u32(c, c->hist, (u64)a.B * a.G));
     if (small) k_ss_scatter<true><<<a.G, SS_NT, 0, c->stream>>>(a);
-    else k_ss_scatter<false><<<a.G, SS_NT, 0, c->stream>>>(a);
+    else k_ss_scatter<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
     k_ss_bucket<<<a.B, SB_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
     if (c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA));
@@ -572,7 +575,7 @@ int wcg_close(wcg_ctx* c) {
     }
     void* bufs[] = {c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens, c->d_scalar, c->d_out,
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
-                    c->llog, c->llog_len, c->smp, c->bid, c->hist, c->spart, c->ikey, c->iidx, c->groups,
+                    c->llog, c->llog_len, c->smp, c->bid, c->irec, c->lent, c->lpcur, c->hist, c->spart, c->ikey, c->iidx, c->groups,
                     c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
@@ -668,9 +671,9 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         HIPCHK(c, hipMalloc(&c->wg_stats, grid * 4 * sizeof(u64)));
         c->wg_stats_cap = grid;
     }
-    // long-token log: sized for LLOG_PER_STEP records per step on average (C4 text logs ~5.3);
-    // tokens past a full region are counted inline by k_map (long_token: exact, slower), so an
-    // adversarial input costs time, never memory or an error
+    // long-token log: LLOG_PER_STEP records per step, the most a step can start (C4 text logs
+    // ~5.3 per step), so no region fills and k_map needs no inline fallback (an inlined insert
+    // path pushed k_map past its register budget into spills of its prefetch registers)
     a.llog_cap = (u32)std::min<u64>((u64)a.tiles_per_wg * LLOG_PER_STEP + 64, 0xFFFFFFFFull);
     const u64 lneed = grid * (u64)a.llog_cap * sizeof(u64);
     if (lneed > c->llog_cap) {
@@ -707,10 +710,20 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     }
     HIPCHK(c, hipGetLastError());
     if (c->timing) { e1 = take_event(c); HIPCHK(c, hipEventRecord(e1, c->stream)); }
-    // the logged long tokens: LONG_PARTS workgroups per map workgroup's region
+    // the logged long tokens: hashed into LQ partitions (LONG_PARTS workgroups per map
+    // workgroup's region), then one workgroup per partition.  Partition capacity: the log's
+    // capacity spread evenly, with slack (the LDS cache folds hot keys before they are emitted;
+    // a full partition falls back to exact per-entry inserts)
     if (ablate == 0 || ablate >= 6) {
-        static const int lab = getenv("WCG_LONG_ABLATE") ? atoi(getenv("WCG_LONG_ABLATE")) : 0;
-        k_long<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, c->stream>>>(a, (u32)grid, lab);
+        LongPart lp;
+        const u64 expect = grid * (u64)a.tiles_per_wg * 16;     // 16 per step: 3x C4's rate
+        lp.cap = (u32)std::min<u64>(std::max<u64>(1024, (expect * 5 / 4 + LQ - 1) / LQ), 0x7FFFFFFFull);
+        RC(ensure(c, &c->lent, &c->lent_cap, (u64)LQ * lp.cap));
+        RC(ensure(c, &c->lpcur, &c->lpcur_cap, (u64)LQ));
+        HIPCHK(c, hipMemsetAsync(c->lpcur, 0, LQ * sizeof(u32), c->stream));
+        lp.ent = c->lent; lp.cur = c->lpcur;
+        k_long_hash<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, c->stream>>>(a, lp, (u32)grid);
+        k_long_agg<<<LQ, LONG_NT, 0, c->stream>>>(a, lp);
         HIPCHK(c, hipGetLastError());
     }
     AggArgs g;

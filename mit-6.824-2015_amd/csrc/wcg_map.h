@@ -25,10 +25,11 @@
 //
 // Prefetch accounting.  `s_waitcnt vmcnt(N)` waits until all but this wave's N youngest vector
 // memory operations are done (loads and stores retire in issue order).  A step's processing
-// issues exactly 2 miss-log stores per token iteration plus 2 after its last one (inline-asm
-// buffer stores executed by the whole wave, out-of-range offsets for lanes without a miss), so
-// when set s is due the number of operations issued after its loads is known: the other sets'
-// MAP_SETS - 1 loads + 2 * (iters + 1) for each of the MAP_SETS - 1 steps processed since.  The
+// issues exactly 1 miss-log store per short-key iteration and 2 per general iteration, plus 2
+// after its last one (inline-asm buffer stores executed by the whole wave, out-of-range offsets
+// for lanes without a miss), so when set s is due the number of operations issued after its
+// loads is known: the other sets' MAP_SETS - 1 loads + the stores of each of the MAP_SETS - 1
+// steps processed since.  The
 // wait uses the largest quantised N not above that count; any operation the count does not know about (rare paths: long tokens, a full miss-log
 // region, UTF-8 table loads) can only make the wait stronger.
 #pragma once
@@ -59,11 +60,11 @@ constexpr int MAP_SETS = WCG_MAP_SETS;       // steps in flight per wave (2 or 4
 #ifndef WCG_MASKED_RESERVE
 #define WCG_MASKED_RESERVE 0                 // 1: miss reservations by the missing lanes only
 #endif
+#ifndef WCG_WAIT0
+#define WCG_WAIT0 0                          // diagnostics: 1 = wait for every older memory op
+#endif
 #ifndef WCG_NOWAIT
 #define WCG_NOWAIT 0                         // diagnostics: 1 = never wait for the window loads
-#endif
-#ifndef WCG_PIPE
-#define WCG_PIPE 1                           // token-loop pipeline depth (1 or 2)
 #endif
 constexpr int MAX_MISS_BUCKETS = 256;
 constexpr u32 SST_LEN_SHIFT = 10;            // start entry = window offset | min(run, 16) << 10
@@ -85,7 +86,9 @@ struct MapArgs {
     u32* llog_len;                 // records written per region
 };
 constexpr u64 LLOG_OFF_MASK = (1ull << 40) - 1;   // record = input offset | len << 40 (len 0: walk)
-constexpr u32 LLOG_PER_STEP = 16;                 // long-token log records per step (average)
+constexpr u32 LLOG_PER_STEP = 64;                 // long-token log records per step: a bound (a
+                                                  // step's 992 bytes start at most 59 tokens of
+                                                  // 16+ bytes), so a region never fills
 
 // append one miss-log entry (wcg_lds_table.h) for this workgroup; false when the region is
 // full (the units of a region's last, cut-off entry are zeroed so k_agg skips them)
@@ -117,22 +120,29 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t* in, u64 n, long pos) 
     return v;
 }
 
-// count one long key (> 15 bytes: len, FNV-1a 64 h over its bytes) in the long-key table;
-// w(j) returns key word j (little-endian bytes 4j..4j+3, zeros past len).  Key bytes are
-// written and compared 16 bytes at a time against the zero-padded arena cells (wcg_common.h):
-// a byte loop over global memory is a chain of dependent loads per byte.
-// Returns the slot that counted the key + 1 (0 when nothing was counted) and its arena offset.
+__device__ __forceinline__ u64 long_tag(u64 h, u64 len) { return mix64(h ^ len) | 1ull; }
+
+// count c occurrences of one long key (> 15 bytes; tag = long_tag(FNV-1a 64 of its bytes, len))
+// in the long-key table; w(j) returns key word j (little-endian bytes 4j..4j+3, zeros past len).
+// Key bytes are written and compared 16 bytes at a time against the zero-padded arena cells
+// (wcg_common.h): a byte loop over global memory is a chain of dependent loads per byte.
+// Publication: `fenced` (any key, any workgroup, concurrently): the arena bytes are released
+// before k1 publishes them and acquired before they are compared.  Unfenced (k_long_agg's flush):
+// within one launch a key reaches the table from ONE workgroup only (its partition's), so the
+// only writer a reader can race is its own workgroup - same CU, same L2 - and the bytes are
+// compared with L1-bypassing loads; an agent-scope fence per key wrote back the whole XCD L2
+// (~2-6 us) and made the old per-occurrence k_long take 8.8 ms on 1 GiB of C4.
+// Returns the slot that counted the key + 1 (0 when nothing was counted).
 template <typename W>
-__device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 h, W w, int mode = 0, u64* arena_off = nullptr) {
+__device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 tag, W w, u64 c, bool fenced) {
     if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); return 0; }
-    u64 tag = mix64(h ^ len) | 1ull;
     u64 s = tag & a.lmask, probes = 0;
     int spins = 0;
     while (true) {
         GEntry* e = &a.ltab[s];
         // the entry's three words in one round trip (independent loads); aux (the length) is
-        // written once, before the release that publishes k1: a 0 read here is re-read after
-        // the acquire, any other value is final
+        // written once, before k1 is published: a 0 read here is re-read after k1, any other
+        // value is final
         u64 c0 = ld_agent(&e->k0);
         u64 r = ld_agent(&e->k1);
         u64 elen = ld_agent(&e->aux);
@@ -146,10 +156,10 @@ __device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 h, W w, i
                     *reinterpret_cast<uint4*>(a.arena + off + j) =
                         make_uint4(w(j / 4), w(j / 4 + 1), w(j / 4 + 2), w(j / 4 + 3));
                 st_agent(&e->aux, len);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                if (fenced) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(&e->k1, off + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                add_agent(&e->cnt, 1);
-                if (arena_off) *arena_off = off;
+                add_agent(&e->cnt, c);
                 return s + 1;
             }
             c0 = exp;
@@ -160,20 +170,21 @@ __device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 h, W w, i
                 if (++spins > SPIN_LIMIT) { atomicAdd(&a.st->spin_fail, 1u); return 0; }
                 continue;
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (fenced) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             if (elen == 0) elen = ld_agent(&e->aux);
             bool same = elen == len;
             if (same) {                 // 16-byte cells, zero-padded on both sides
                 u32 diff = 0;
                 for (u64 j = 0; j < len; j += 16) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(a.arena + r - 1 + j);
-                    diff |= (v.x ^ w(j / 4)) | (v.y ^ w(j / 4 + 1)) | (v.z ^ w(j / 4 + 2)) | (v.w ^ w(j / 4 + 3));
+                    const u64* q = reinterpret_cast<const u64*>(a.arena + r - 1 + j);
+                    const u64 v0 = fenced ? q[0] : ld_agent(q), v1 = fenced ? q[1] : ld_agent(q + 1);
+                    diff |= ((u32)v0 ^ w(j / 4)) | ((u32)(v0 >> 32) ^ w(j / 4 + 1)) | ((u32)v1 ^ w(j / 4 + 2)) |
+                            ((u32)(v1 >> 32) ^ w(j / 4 + 3));
                 }
                 same = diff == 0;
             }
             if (same) {
-                if (mode != 2) add_agent(&e->cnt, 1);
-                if (arena_off) *arena_off = r - 1;
+                add_agent(&e->cnt, c);
                 return s + 1;
             }
         }
@@ -182,11 +193,10 @@ __device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 h, W w, i
     }
 }
 
-// long token (> 15 bytes, or a run k_map could not measure in its window) starting at absolute
-// offset p: walk runes in global memory
-__device__ void long_token(const MapArgs& a, u64 p) {
+// length of the letter run at absolute offset p (walking runes in global memory), its FNV-1a 64
+__device__ u64 long_walk(const MapArgs& a, u64 p, u64* hash) {
     const uint8_t* in = a.in;
-    u64 n = a.n;
+    const u64 n = a.n;
     auto at = [&](long i) -> u32 { return (i >= 0 && (u64)i < n) ? in[i] : 0u; };
     u64 q = p;
     u64 h = 0xCBF29CE484222325ull;
@@ -197,26 +207,45 @@ __device__ void long_token(const MapArgs& a, u64 p) {
         for (int k = 0; k < w; k++) { h ^= in[q + k]; h *= 0x100000001B3ull; }
         q += w;
     }
-    u64 len = q - p;
-    if (len <= 15) {
-        // a run k_map could not measure inside its window (a UTF-8 look-ahead chunk) that turns
-        // out to be an inline key: count it in the inline-key table like any other
-        u64 b0 = 0, b1 = 0;
-        for (u64 i = 0; i < len; i++) {
-            if (i < 8) b0 |= (u64)in[p + i] << (8 * i);
-            else b1 |= (u64)in[p + i] << (8 * (i - 8));
-        }
-        u64 k0, k1;
-        make_key(b0, b1, (int)len, k0, k1);
-        ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
-        return;
+    *hash = h;
+    return q - p;
+}
+
+// a run that turned out to be an inline key (<= 15 bytes: measured only after a rune walk)
+__device__ __forceinline__ void count_inline_run(const MapArgs& a, u64 p, u64 len) {
+    u64 b0 = 0, b1 = 0;
+    for (u64 i = 0; i < len; i++) {
+        if (i < 8) b0 |= (u64)a.in[p + i] << (8 * i);
+        else b1 |= (u64)a.in[p + i] << (8 * (i - 8));
     }
-    ltab_add(a, len, h, [&](u64 j) -> u32 {
-        u32 v = 0;
-        for (u64 k = 0; k < 4; k++)
-            if (4 * j + k < len) v |= (u32)in[p + 4 * j + k] << (8 * k);
-        return v;
-    });
+    u64 k0, k1;
+    make_key(b0, b1, (int)len, k0, k1);
+    ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
+}
+
+// key word j (little-endian bytes 4j..4j+3 of the key at input offset p, zeros past len) from
+// the resident input: two aligned loads + alignbyte
+__device__ __forceinline__ u32 input_word(const MapArgs& a, u64 p, u32 len, u64 j) {
+    if (4 * (u32)j >= len) return 0u;
+    const u64 base = p + 4 * j, q = base & ~3ull;
+    const u32 rem = len - 4 * (u32)j;
+    u32 v;
+    if (q + 8 <= a.n) {
+        const u32* wq = reinterpret_cast<const u32*>(a.in + q);
+        v = __builtin_amdgcn_alignbyte(wq[1], wq[0], (u32)(base & 3));
+    } else {
+        v = 0;
+        for (u32 b = 0; b < 4 && b < rem; b++) v |= (u32)a.in[base + b] << (8 * b);
+    }
+    return rem >= 4 ? v : v & ((1u << (8 * rem)) - 1);
+}
+
+// do the long keys at input offsets p and q (both len bytes) have the same bytes?
+__device__ __forceinline__ bool input_same(const MapArgs& a, u64 p, u64 q, u32 len) {
+    if (p == q) return true;
+    u32 diff = 0;
+    for (u64 j = 0; 4 * j < len && diff == 0; j++) diff |= input_word(a, p, len, j) ^ input_word(a, q, len, j);
+    return diff == 0;
 }
 
 // long token (> 15 bytes) starting at window offset rp (absolute offset p): its length from the
@@ -240,111 +269,159 @@ __device__ __forceinline__ void long_token_log(const MapArgs& a, u64 p, u32 rp, 
     if (ABL == 7) { asm volatile("" ::"v"(len)); return; }
     const u32 pos = atomicAdd(lcur, 1u);
     if (pos < a.llog_cap) a.llog[(u64)blockIdx.x * a.llog_cap + pos] = p | (u64)len << 40;
-    else long_token(a, p);              // region full (dense long tokens): count it here, exactly
+    else atomicAdd(&a.st->overflow, 1u);   // cannot happen (LLOG_PER_STEP); fails loudly if it does
 }
 
-// k_long: count the logged long tokens in the long-key table.  Workgroup b serves map region
-// b % nreg, with its LONG_PARTS workgroups striding over the region's records in rounds of
-// LONG_NT.  Key words come from the resident input (two aligned loads + alignbyte, bytes past
-// the key masked to zero).
-// Hot keys: one count atomic per occurrence serialises on the key's slot (C4: the top long key
-// occurs 1.2e5 times per GiB; the count atomics were 5 of k_long's 12 ms).  A workgroup caches
-// {tag, len, slot, arena offset} of the keys it has counted in LDS; an occurrence whose tag and
-// length match a cached key compares its bytes with the key's arena cell (exact, 16-byte loads)
-// and counts in LDS; the LDS counts are added to the table once at the end.  A lane never waits
-// on another's LDS write: an entry being filled in the same round may be seen half-written (tag
-// set, offset still 0 or length stale), and such a probe simply falls through to ltab_add.
-// Correctness rests on the exact match (tag, length, then the key's bytes against its real arena
-// cell, with coff == 0 treated as "not filled"), not on when entries become visible; cslot is
-// read only after the final barrier.
+// ---- long keys: k_long_hash -> k_long_agg.  Every occurrence of a long key is routed, by its
+//      tag, to one of LQ partitions, so ONE workgroup aggregates all of a key's occurrences in
+//      LDS (exact: bytes compared against a representative occurrence in the resident input) and
+//      adds the key to the long-key table once, unfenced.  The per-occurrence table inserts of a
+//      flat design serialise on hot keys and on the fences that publish arena bytes across CUs.
+constexpr u32 LQ = 2048;                      // partitions
+struct LEnt { u64 h; u64 rec; u64 cnt; };     // FNV-1a 64, input offset | len << 40, occurrences
+struct LongPart { LEnt* ent; u32* cur; u32 cap; };
+__device__ __forceinline__ u32 long_part(u64 tag) { return (u32)(tag >> 40) & (LQ - 1); }
+
+// k_long_hash: workgroup b reads map region b % nreg (its LONG_PARTS workgroups stride over the
+// region's records in rounds of LONG_NT), hashes each logged token from the resident input
+// (walking runes for records of length 0) and emits {h, rec, count} to the token's partition.
+// Repeats are pre-aggregated in an LDS cache keyed by tag (hot keys: C4's top long key occurs
+// 1.2e5 times per GiB), compared byte-exactly against the cached occurrence's input bytes - no
+// other CU's writes are read, so no fence is needed.  A lane never waits on another's LDS write:
+// a cache entry claimed in the same round may still have no representative (rec 0), and such a
+// lane simply emits its own entry.  A full partition falls back to a fenced table insert.
 constexpr int LONG_NT = 256;
 constexpr int LONG_PARTS = 8;
-constexpr int LCACHE = 1024;                  // LDS cache entries (28 B each)
-// mode (measurement only, WCG_LONG_ABLATE; results are wrong when mode != 0): 1 = hash only,
-// 2 = no count atomic on a hit, 3 = no LDS cache
-__global__ __launch_bounds__(LONG_NT) void k_long(MapArgs a, u32 nreg, int mode) {
+constexpr int LCACHE = 1024;                  // LDS cache entries (20 B each)
+__global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u32 nreg) {
     __shared__ u64 ctag[LCACHE];
-    __shared__ u64 coff[LCACHE];              // arena offset + 1 (0 = not filled)
-    __shared__ u32 cslot[LCACHE], clen[LCACHE], ccnt[LCACHE];
+    __shared__ u64 crec[LCACHE];              // representative occurrence (0 = not yet set)
+    __shared__ u32 ccnt[LCACHE];
     const u32 reg = blockIdx.x % nreg, part = blockIdx.x / nreg;
     const u32 nrec = a.llog_len[reg];
     const u64* recs = a.llog + (u64)reg * a.llog_cap;
     const u32 stride = LONG_PARTS * LONG_NT, first = part * LONG_NT;
     const u32 rounds = nrec > first ? (nrec - first + stride - 1) / stride : 0;   // workgroup-uniform
     if (rounds == 0) return;          // ASCII text: nearly every workgroup (no barrier reached yet)
-    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; coff[e] = 0; ccnt[e] = 0; clen[e] = 0; }
+    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; crec[e] = 0; ccnt[e] = 0; }
     __syncthreads();
-    const uint8_t* in = a.in;
-    const u64 n = a.n;
+    auto emit = [&](u64 h, u64 rec, u64 c) {
+        const u64 len = rec >> 40, p = rec & LLOG_OFF_MASK;
+        const u32 q = long_part(long_tag(h, len));
+        const u32 pos = atomicAdd(&lp.cur[q], 1u);
+        if (pos < lp.cap) {
+            LEnt* d = lp.ent + (u64)q * lp.cap + pos;
+            d->h = h; d->rec = rec; d->cnt = c;
+        } else {                      // partition full: count it here (fenced, exact)
+            ltab_add(a, len, long_tag(h, len), [&](u64 j) -> u32 { return input_word(a, p, (u32)len, j); }, c, true);
+        }
+    };
     for (u32 k = 0; k < rounds; k++) {
         const u32 i = first + k * stride + threadIdx.x;
         const u64 r = i < nrec ? recs[i] : 0;
         const u64 p = r & LLOG_OFF_MASK;
-        const u32 len = (u32)(r >> 40);
-        if (i < nrec && len == 0) long_token(a, p);
-        if (len != 0) {
-            auto word = [&](u64 j) -> u32 {
-                if (4 * (u32)j >= len) return 0u;
-                const u64 base = p + 4 * j, q = base & ~3ull;
-                const u32 rem = len - 4 * (u32)j;
-                u32 v;
-                if (q + 8 <= n) {
-                    const u32* wq = reinterpret_cast<const u32*>(in + q);
-                    v = __builtin_amdgcn_alignbyte(wq[1], wq[0], (u32)(base & 3));
-                } else {
-                    v = 0;
-                    for (u32 b = 0; b < 4 && b < rem; b++) v |= (u32)in[base + b] << (8 * b);
-                }
-                return rem >= 4 ? v : v & ((1u << (8 * rem)) - 1);
-            };
-            u64 h = 0xCBF29CE484222325ull;
+        u64 len = r >> 40, h = 0;
+        if (i < nrec && len == 0) {
+            len = long_walk(a, p, &h);
+            if (len <= 15) { count_inline_run(a, p, len); len = 0; }
+            else if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); len = 0; }
+        } else if (len != 0) {
+            h = 0xCBF29CE484222325ull;
             for (u32 j = 0; 4 * j < len; j++) {
-                const u32 v = word(j);
-                const u32 nb = len - 4 * j < 4 ? len - 4 * j : 4;
+                const u32 v = input_word(a, p, (u32)len, j);
+                const u32 nb = len - 4 * j < 4 ? (u32)len - 4 * j : 4;
                 for (u32 b = 0; b < nb; b++) { h ^= (v >> (8 * b)) & 0xFFu; h *= 0x100000001B3ull; }
             }
-            if (mode == 1) { if (h == 0) atomicAdd(&a.st->overflow, 1u); }
-            else {
-                const u64 tag = mix64(h ^ len) | 1ull;
-                const u32 c0 = (u32)(tag >> 24) & (LCACHE - 1);
-                bool done = false;
-                if (mode == 0) {
-                    for (u32 q = 0; q < 4; q++) {                 // cached keys (earlier rounds)
-                        const u32 cs = (c0 + q) & (LCACHE - 1);
-                        const u64 t = ctag[cs];
-                        if (t == 0) break;
-                        if (t != tag) continue;
-                        const u64 off = coff[cs];
-                        if (off == 0 || clen[cs] != len) continue;
-                        u32 diff = 0;
-                        for (u64 j = 0; j < len; j += 16) {
-                            const uint4 v = *reinterpret_cast<const uint4*>(a.arena + off - 1 + j);
-                            diff |= (v.x ^ word(j / 4)) | (v.y ^ word(j / 4 + 1)) | (v.z ^ word(j / 4 + 2)) | (v.w ^ word(j / 4 + 3));
-                        }
-                        if (diff == 0) { atomicAdd(&ccnt[cs], 1u); done = true; }
-                        break;
-                    }
+        }
+        if (len != 0) {
+            const u64 tag = long_tag(h, len), rec = p | len << 40;
+            const u32 c0 = (u32)(tag >> 24) & (LCACHE - 1);
+            bool done = false;
+            for (u32 q = 0; q < 4 && !done; q++) {
+                const u32 cs = (c0 + q) & (LCACHE - 1);
+                u64 t = ctag[cs];
+                if (t == 0) {
+                    t = atomicCAS((unsigned long long*)&ctag[cs], 0ull, (unsigned long long)tag);
+                    if (t == 0) { crec[cs] = rec; atomicAdd(&ccnt[cs], 1u); done = true; break; }
                 }
-                if (!done) {
-                    u64 off = 0;
-                    const u64 s1 = ltab_add(a, len, h, word, mode, &off);
-                    if (mode == 0 && s1) {                         // cache it for later rounds
-                        for (u32 q = 0; q < 4; q++) {
-                            const u32 cs = (c0 + q) & (LCACHE - 1);
-                            const u64 t = atomicCAS((unsigned long long*)&ctag[cs], 0ull, (unsigned long long)tag);
-                            if (t == 0) { coff[cs] = off + 1; cslot[cs] = (u32)(s1 - 1); clen[cs] = len; break; }
-                            if (t == tag) break;
-                        }
-                    }
+                if (t != tag) continue;
+                const u64 rr = crec[cs];
+                if (rr != 0 && (rr >> 40) == len && input_same(a, p, rr & LLOG_OFF_MASK, (u32)len)) {
+                    atomicAdd(&ccnt[cs], 1u);
+                    done = true;
                 }
+                break;                // same tag, other key or not yet set: emit
+            }
+            if (!done) emit(h, rec, 1);
+        }
+        __syncthreads();              // this round's representatives are visible to the next
+    }
+    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) {
+        const u64 rr = crec[e];
+        if (rr == 0 || ccnt[e] == 0) continue;
+        const u64 len = rr >> 40, p = rr & LLOG_OFF_MASK;
+        u64 h = 0xCBF29CE484222325ull;
+        for (u32 j = 0; 4 * j < len; j++) {
+            const u32 v = input_word(a, p, (u32)len, j);
+            const u32 nb = len - 4 * j < 4 ? (u32)len - 4 * j : 4;
+            for (u32 b = 0; b < nb; b++) { h ^= (v >> (8 * b)) & 0xFFu; h *= 0x100000001B3ull; }
+        }
+        emit(h, rr, ccnt[e]);
+    }
+}
+
+// k_long_agg: one workgroup per partition.  Rounds of LONG_NT entries: (1) each entry claims or
+// finds its tag's LDS slot (linear probing) and the claimer stores its occurrence as the slot's
+// representative; barrier; (2) each entry compares its bytes with the representative's and adds
+// its count.  A tag collision between different keys, or a full table, falls back to a fenced
+// table insert of that entry (exact).  Finally every slot is added to the long-key table once.
+constexpr u32 LA_SLOTS = 2048;
+constexpr u32 LA_PROBES = 32;
+__global__ __launch_bounds__(LONG_NT) void k_long_agg(MapArgs a, LongPart lp) {
+    __shared__ u64 stag[LA_SLOTS], srec[LA_SLOTS], scnt[LA_SLOTS], sh[LA_SLOTS];
+    const u32 q = blockIdx.x;
+    const u32 nq = lp.cur[q] < lp.cap ? lp.cur[q] : lp.cap;
+    if (nq == 0) return;
+    for (u32 s = threadIdx.x; s < LA_SLOTS; s += LONG_NT) { stag[s] = 0; srec[s] = 0; scnt[s] = 0; }
+    __syncthreads();
+    const LEnt* E = lp.ent + (u64)q * lp.cap;
+    for (u32 base = 0; base < nq; base += LONG_NT) {
+        const u32 e = base + threadIdx.x;
+        const bool valid = e < nq;
+        LEnt x = {0, 0, 0};
+        if (valid) x = E[e];
+        const u64 len = x.rec >> 40, p = x.rec & LLOG_OFF_MASK;
+        const u64 tag = long_tag(x.h, len);
+        int slot = -1;
+        if (valid) {
+            const u32 s0 = (u32)(tag >> 8) & (LA_SLOTS - 1);
+            for (u32 j = 0; j < LA_PROBES; j++) {
+                const u32 s = (s0 + j) & (LA_SLOTS - 1);
+                u64 t = stag[s];
+                if (t == 0) {
+                    t = atomicCAS((unsigned long long*)&stag[s], 0ull, (unsigned long long)tag);
+                    if (t == 0) { srec[s] = x.rec; sh[s] = x.h; slot = (int)s; break; }
+                }
+                if (t == tag) { slot = (int)s; break; }
             }
         }
         __syncthreads();
-        // the arena cells read from the cache were written by other CUs: drop stale L1 lines
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        bool fallback = valid && slot < 0;
+        if (valid && slot >= 0) {
+            const u64 rr = srec[slot];
+            if ((rr >> 40) == len && input_same(a, p, rr & LLOG_OFF_MASK, (u32)len)) atomicAdd((unsigned long long*)&scnt[slot], (unsigned long long)x.cnt);
+            else fallback = true;
+        }
+        if (fallback)
+            ltab_add(a, len, tag, [&](u64 j) -> u32 { return input_word(a, p, (u32)len, j); }, x.cnt, true);
+        __syncthreads();              // slots claimed in the next round cannot be confused with ...
+    }                                 // ... representatives read in this one
+    for (u32 s = threadIdx.x; s < LA_SLOTS; s += LONG_NT) {
+        const u64 c = scnt[s];
+        if (c == 0) continue;
+        const u64 rr = srec[s], len = rr >> 40, p = rr & LLOG_OFF_MASK;
+        ltab_add(a, len, long_tag(sh[s], len), [&](u64 j) -> u32 { return input_word(a, p, (u32)len, j); }, c, false);
     }
-    for (int e = threadIdx.x; e < LCACHE; e += LONG_NT)
-        if (ccnt[e]) add_agent(&a.ltab[cslot[e]].cnt, (u64)ccnt[e]);
 }
 
 // wave-local ordering of LDS accesses between lanes (the LDS executes one wave's
@@ -485,7 +562,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         return t;
     };
 
-    // one step: returns the number of unit-store pairs it issued (prefetch accounting)
+    // one step: returns the number of unit stores it issued (prefetch accounting)
     auto process = [&](u64 step, const uint4 mine) -> u32 {
         const long wbase = (long)(step * MAP_STEP) - 16;        // input offset of window byte 0
         if (ABL == 5) { asm volatile("" ::"v"(mine.x)); return 0; }
@@ -550,18 +627,18 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         //      the entry after that.  A miss reserves its units with an LDS atomic whose result
         //      is read one iteration later (after that iteration's probe reads have returned, so
         //      the reservation adds no round trip of its own), and the wave stores the units
-        //      then: 2 unit stores per iteration + 2 after the loop (prefetch accounting)
+        //      then: 1 unit store per short iteration, 2 per general iteration, 2 after the loop
+        //      (prefetch accounting)
         u32 sink = 0;
         bool missp = false;                   // the previous iteration's miss: bucket, units,
         u32 pp = 0, nup = 0, posp = 0;        // reservation and key
         u64 k0p = 0, k1p = 0;
         const u32 rcap = (u32)a.region_cap;   // < 2^22 (host), so offsets fit 24-bit multiplies
-        auto store_pending = [&]() {
+        auto store_pending = [&](bool two) {
             const bool fits = missp && posp + nup <= rcap;
             const u32 o0 = fits ? (__umul24(pp, rcap) + posp) * 8u : OOB;
-            const u32 o1 = fits && nup == 2 ? o0 + 8u : OOB;
             unit_store(prsrc, o0, k0p);
-            unit_store(prsrc, o1, k1p);
+            if (two) unit_store(prsrc, fits && nup == 2 ? o0 + 8u : OOB, k1p);
             if (missp && !fits) {             // region full: zero its tail, global table
                 u64* r = wpool + (u64)pp * a.region_cap;
                 for (u32 k = posp; k < rcap; k++) r[k] = 0;
@@ -574,8 +651,10 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         const u32 nsh = (ABL == 0 || ABL >= 6) ? (tot_s >> 6) : 0u;
         const u32 first = nsh * 64;
         const u32 iters = (total - first + 63) >> 6;
-        // one software pipeline over both loops: the short loop's last iteration reads and decodes
-        // the general loop's first token, and neither loop decodes past its last iteration
+        // Each loop is software-pipelined on its own; reads and decodes past a loop's last
+        // iteration are unconditional and unused (entries past the list read other LDS words,
+        // key reads stay inside the wave's staging bytes), so no loop-carried state is merged
+        // across loop-exit branches.
         Tok cur;
         u32 e_nxt;
         if (nsh) {
@@ -601,16 +680,13 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             TokS cs = decode_s(sst[lane], keyread_s(sst[lane]));
             e_nxt = sst[64 + lane];
             for (u32 it = 0; it < nsh; it++) {
-                const bool more = it + 1 < nsh;                        // wave-uniform
                 const auto pr = tab.probe_short(cs.h);
-                uint4 nks;
-                KeyWords nkg;
-                if (more) nks = keyread_s(e_nxt);
-                else if (iters) nkg = keyread(e_nxt);                 // the general loop's first token
+                const uint4 nks = keyread_s(e_nxt);
                 const u32 e_nn = sst[(it + 2) * 64 + lane];
+                __builtin_amdgcn_sched_barrier(0);  // all three reads issue before the probe's wait
                 const bool hit = tab.finish_short(cs.k, cs.h, pr);
                 my_hits += (u32)hit;
-                store_pending();
+                store_pending(false);         // short keys: one unit
                 missp = !hit;
                 pp = miss_bucket(cs.h, a.pmask);
                 nup = 1u;
@@ -620,17 +696,19 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
                 posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
 #endif
                 k0p = cs.k; k1p = 0;
-                if (more) cs = decode_s(e_nxt, nks);
-                else if (iters) cur = decode_tok(e_nxt, first + lane < total, nkg);
+                cs = decode_s(e_nxt, nks);
                 e_nxt = e_nn;
             }
+            e_nxt = sst[first + lane];
         } else {
-            cur = decode_tok(sst[lane], lane < total, keyread(sst[lane]));
-            e_nxt = sst[64 + lane];
+            e_nxt = sst[lane];
+        }
+        if (iters) {
+            cur = decode_tok(e_nxt, first + lane < total, keyread(e_nxt));
+            e_nxt = sst[first + 64 + lane];
         }
         for (u32 it = 0; it < iters; it++) {
             const u32 base = first + it * 64;
-            const bool more = it + 1 < iters;                          // wave-uniform
             if (ABL == 1) { sink += cur.e; cur.e = sst[base + 64 + lane]; continue; }
             if (cur.lng) {
                 my_long++;
@@ -643,13 +721,13 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
                             e_nxt = sst[base + 128 + lane]; continue; }
             // issue together: this token's probe, the next token's key bytes, the entry after
             const auto pr = tab.probe(med, cur.h);
-            KeyWords nkw;
-            if (more) nkw = keyread(e_nxt);
+            const KeyWords nkw = keyread(e_nxt);
             const u32 e_nn = sst[base + 128 + lane];
+            __builtin_amdgcn_sched_barrier(0);
             const bool hit = tab.finish(cur.valid, med, k0, k1, cur.h, pr);
-            if (ABL == 3) { sink += hit; if (more) cur = decode_tok(e_nxt, base + 64 + lane < total, nkw); e_nxt = e_nn; continue; }
+            if (ABL == 3) { sink += hit; cur = decode_tok(e_nxt, base + 64 + lane < total, nkw); e_nxt = e_nn; continue; }
             my_hits += (u32)hit;
-            store_pending();                  // the previous iteration's miss units
+            store_pending(true);              // the previous iteration's miss units
             // this token's miss: reserve units in the (workgroup, bucket) region
             missp = cur.valid && !hit;
             pp = miss_bucket(cur.h, a.pmask);
@@ -660,18 +738,18 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             posp = atomicAdd(&cursor[pp], missp ? nup : 0u);   // every lane (0 = no miss)
 #endif
             k0p = k0; k1p = k1;
-            if (more) cur = decode_tok(e_nxt, base + 64 + lane < total, nkw);
+            cur = decode_tok(e_nxt, base + 64 + lane < total, nkw);
             e_nxt = e_nn;
         }
-        if (ABL == 0 || ABL >= 6) store_pending();
+        if (ABL == 0 || ABL >= 6) store_pending(true);
         if (ABL) asm volatile("" ::"v"(sink));
         wave_lds_sync();
-        return (ABL == 0 || ABL >= 6) ? nsh + iters + 1 : 0u;
+        return (ABL == 0 || ABL >= 6) ? nsh + 2 * (iters + 1) : 0u;
     };
 
     // ---- main loop, unrolled over the register sets so that each set's load and waits name
     //      fixed registers (tools/check_inflight.py); a set's load was issued MAP_SETS steps
-    //      earlier; h1..h3 = unit-store pairs of the last three steps (the wait count)
+    //      earlier; h1..h3 = unit stores of the last three steps (the wait count)
     auto is_tail = [&](u64 step) { return step * MAP_STEP - 16 + MAP_WIN > a.n; };
     auto u4 = [](v4u v) { return make_uint4(v.x, v.y, v.z, v.w); };
     v4u mA, mB, mC, mD;
@@ -692,7 +770,8 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         v4i r; u32 om;                                                                          \
         addr(st + MAP_SETS * stride, r, om);                                                    \
         if (WCG_NOWAIT) set_wait_##S(63, m##S); /* diagnostics only: results are wrong */       \
-        else set_wait_##S((MAP_SETS - 1) + 2 * (h1 + (MAP_SETS == 4 ? h2 + h3 : 0)), m##S);     \
+        else if (WCG_WAIT0) set_wait_##S(0, m##S);                                              \
+        else set_wait_##S((MAP_SETS - 1) + h1 + (MAP_SETS == 4 ? h2 + h3 : 0), m##S);           \
         const u32 it_ = process(st, u4(m##S));                                                  \
         set_load_##S(r, om, m##S);                                                              \
         h3 = h2; h2 = h1; h1 = it_;                                                             \

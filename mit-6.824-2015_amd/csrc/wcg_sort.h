@@ -25,6 +25,39 @@ __device__ __forceinline__ bool key3_lt(u64 ah, u64 al, u32 ai, u64 bh, u64 bl, 
     return ah < bh || (ah == bh && (al < bl || (al == bl && ai < bi)));
 }
 
+// ---------------------------------------------------------------- LDS bitonic network
+// Sorts P (a power of two) entries (hi, lo, pos) in LDS by that triple, NT threads.  Thread t
+// takes compare-exchange pairs t, t + NT, ...; a block of 64 consecutive pairs belongs to one wave
+// and, for compare distances j <= 64, touches only its own 128 entries - so those stages (most of
+// the network: 49 of 55 for P = 1024) are ordered by a wave barrier, and only stages with
+// j >= 128 pay a workgroup barrier.  The caller's __syncthreads precedes and follows the call.
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int NT>
+__device__ __forceinline__ void lds_bitonic(u64* kh, u64* kl, uint16_t* kp, u32 P) {
+    const u32 tid = threadIdx.x;
+    for (u32 k = 2; k <= P; k <<= 1)
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+            const bool wide = j >= 128;
+            if (wide) __syncthreads();
+            for (u32 t = tid; t < P / 2; t += NT) {
+                const u32 i = 2 * t - (t & (j - 1)), p = i + j;
+                const u64 ah = kh[i], al = kl[i], bh = kh[p], bl = kl[p];
+                const uint16_t ai = kp[i], bi = kp[p];
+                if (key3_lt(bh, bl, bi, ah, al, ai) == ((i & k) == 0)) {
+                    kh[i] = bh; kl[i] = bl; kp[i] = bi;
+                    kh[p] = ah; kl[p] = al; kp[p] = ai;
+                }
+            }
+            if (wide) __syncthreads();
+            else wave_sync_lds();
+        }
+}
+
 // ---------------------------------------------------------------- merge sort (the sample, runs)
 // k_tile_sort orders each 2048-record tile by an LDS bitonic network, stable (ties by position),
 // then k_merge passes double the run length (A first on equal prefixes: stable).  A stable sort
@@ -50,22 +83,8 @@ __global__ __launch_bounds__(TS_NT) void k_tile_sort(const Rec* in, Rec* out, u6
         si[i] = (uint16_t)i;
     }
     __syncthreads();
-    for (int k = 2; k <= TS_TILE; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-            for (int q = 0; q < TS_TILE / 2 / TS_NT; q++) {
-                const int t = q * TS_NT + tid;               // compare-exchange pair t
-                const int i = 2 * t - (t & (j - 1)), p = i + j;
-                const u64 ah = sh[i], al = sl[i], bh = sh[p], bl = sl[p];
-                const uint16_t ai = si[i], bi = si[p];
-                if (key3_lt(bh, bl, bi, ah, al, ai) == ((i & k) == 0)) {
-                    sh[i] = bh; sl[i] = bl; sh[p] = ah; sl[p] = al;
-                    si[i] = bi; si[p] = ai;
-                }
-            }
-            __syncthreads();
-        }
-    }
+    lds_bitonic<TS_NT>(sh, sl, si, TS_TILE);
+    __syncthreads();
     for (int k = 0; k < TS_TILE / TS_NT; k++) {
         const int i = k * TS_NT + tid;
         if (base + i < n) out[base + i] = in[base + si[i]];
@@ -288,16 +307,15 @@ __global__ __launch_bounds__(SC_NT) void k_scan_apply1(u32* v, u64 m) {
 #ifndef WCG_SS_OVS
 #define WCG_SS_OVS 8
 #endif
-#ifndef WCG_SB_NT
-#define WCG_SB_NT 256
-#endif
 constexpr u32 SS_TARGET = WCG_SS_TARGET;  // expected records per bucket (small buckets: many
                                           // workgroups sort at once, each bitonic network short)
-constexpr u32 SS_CAP = 4096;           // bucket size sorted in LDS (larger: the global path)
 constexpr u32 SS_OVS = WCG_SS_OVS;     // samples per bucket
 constexpr u32 SS_MAXB = 32768;         // buckets (k_ss_hist / k_ss_scatter LDS: 4 B each)
-constexpr int SS_NT = 256;             // hist / scatter workgroups
-constexpr int SB_NT = WCG_SB_NT;       // bucket sort workgroups
+constexpr int SS_NT = 256;             // hist / scatter workgroups, up to SS_LDSB buckets
+constexpr int SSL_NT = 1024;           // hist / scatter workgroups above SS_LDSB buckets
+constexpr u32 SS_TOP = 1024;           // top-level splitters staged in LDS above SS_LDSB buckets
+constexpr u32 SB_CAP = 2048;           // bucket records sorted in LDS (18 B each: 36 KiB)
+constexpr int SB_NT = 256;             // bucket sort workgroups
 
 struct SortArgs {
     const Rec* rec;          // compacted records (index = position)
@@ -308,10 +326,8 @@ struct SortArgs {
     u32 G;                   // hist/scatter workgroups
     u32* bid;                // bucket of every record
     u32* hist;               // [B][G] counts -> exclusive offsets (bucket-major)
-    uint4* ikey;             // items by bucket: {lo.x, lo.y, hi.x, hi.y} (hi, lo)
-    u32* iidx;               // record index of each item
-    uint4* ikey2;            // scratch of the global (oversized bucket) path
-    u32* iidx2;
+    Rec* irec;               // records by bucket (n) ...
+    Rec* irec2;              // ... and the scratch of the oversized-bucket path (n)
     Rec* out;                // sorted records
 };
 
@@ -327,59 +343,77 @@ __global__ void k_ss_sample(SortArgs a, Rec* smp) {
     smp[j] = s;
 }
 
-// splitter b (0 <= b < B - 1) = sample (b + 1) * S / B; bucket(x) = number of splitters <= x
-__device__ __forceinline__ u32 ss_bucket(const SortArgs& a, u64 hi, u64 lo, u32 idx) {
-    u32 l = 0, h = a.B - 1;
-    while (l < h) {
-        const u32 mid = (l + h) >> 1;
-        const Rec& s = a.smp[(u64)(mid + 1) * a.S / a.B];
-        if (!key3_lt(hi, lo, idx, s.hi, s.lo, (u32)s.cnt)) l = mid + 1; else h = mid;
-    }
-    return l;
-}
+// splitter b (0 <= b < B - 1) = sample (b + 1) * S / B; bucket(x) = number of splitters <= x in
+// the (hi, lo, record index) order - a total order, so equal prefixes spread over buckets
+__device__ __forceinline__ const Rec& ss_splitter(const SortArgs& a, u32 b) { return a.smp[(u64)(b + 1) * a.S / a.B]; }
 
 __device__ __forceinline__ void ss_range(const SortArgs& a, u64& i0, u64& i1) {
     i0 = a.n * blockIdx.x / a.G;
     i1 = a.n * (blockIdx.x + 1) / a.G;
 }
 
-// Up to SS_LDSB buckets the splitters are staged in LDS (a binary search of LDS reads instead of
-// dependent global loads), and the histogram is small: several workgroups fit a CU.
+// Up to SS_LDSB buckets every splitter is staged in LDS (a binary search of LDS reads), and the
+// histogram is small: several workgroups fit a CU.
 constexpr u32 SS_LDSB = 2048;
 
+// Above SS_LDSB buckets (large key counts, C4): SS_TOP evenly spaced splitters in LDS narrow the
+// search to ~B / SS_TOP splitters, and a few dependent (L2-resident) global reads finish it;
+// 1024-thread workgroups keep 16 waves of searches in flight beside the 128 KiB histogram.
+__device__ __forceinline__ u32 ss_top_index(const SortArgs& a, u32 t) { return (u32)((u64)(t + 1) * (a.B - 1) / (SS_TOP + 1)); }
+
 template <bool SMALL>
-__global__ __launch_bounds__(SS_NT) void k_ss_hist(SortArgs a) {
+__device__ __forceinline__ u32 ss_find(const SortArgs& a, u64 hi, u64 lo, u32 idx, const u64* sp_hi, const u64* sp_lo,
+                                       const u32* sp_i) {
+    u32 l = 0, h;
+    if (SMALL) {
+        h = a.B - 1;
+        while (l < h) {
+            const u32 mid = (l + h) >> 1;
+            if (!key3_lt(hi, lo, idx, sp_hi[mid], sp_lo[mid], sp_i[mid])) l = mid + 1; else h = mid;
+        }
+        return l;
+    }
+    u32 tl = 0, th = SS_TOP;                      // top splitters <= x
+    while (tl < th) {
+        const u32 mid = (tl + th) >> 1;
+        if (!key3_lt(hi, lo, idx, sp_hi[mid], sp_lo[mid], sp_i[mid])) tl = mid + 1; else th = mid;
+    }
+    l = tl > 0 ? ss_top_index(a, tl - 1) + 1 : 0;
+    h = tl < SS_TOP ? ss_top_index(a, tl) : a.B - 1;
+    while (l < h) {
+        const u32 mid = (l + h) >> 1;
+        const Rec& s = ss_splitter(a, mid);
+        if (!key3_lt(hi, lo, idx, s.hi, s.lo, (u32)s.cnt)) l = mid + 1; else h = mid;
+    }
+    return l;
+}
+
+template <bool SMALL>
+__global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) {
+    constexpr int NT = SMALL ? SS_NT : SSL_NT;
+    constexpr u32 NSP = SMALL ? SS_LDSB : SS_TOP;
     __shared__ u32 h[SMALL ? SS_LDSB : SS_MAXB];
-    __shared__ u64 sp_hi[SMALL ? SS_LDSB : 1], sp_lo[SMALL ? SS_LDSB : 1];
-    __shared__ u32 sp_i[SMALL ? SS_LDSB : 1];
-    for (u32 b = threadIdx.x; b < a.B; b += SS_NT) {
-        h[b] = 0;
-        if (SMALL && b + 1 < a.B) {
-            const Rec& s = a.smp[(u64)(b + 1) * a.S / a.B];
-            sp_hi[b] = s.hi; sp_lo[b] = s.lo; sp_i[b] = (u32)s.cnt;
+    __shared__ u64 sp_hi[NSP], sp_lo[NSP];
+    __shared__ u32 sp_i[NSP];
+    for (u32 b = threadIdx.x; b < a.B; b += NT) h[b] = 0;
+    for (u32 t = threadIdx.x; t < NSP; t += NT) {
+        const bool live = SMALL ? t + 1 < a.B : true;
+        if (live) {
+            const Rec& s = ss_splitter(a, SMALL ? t : ss_top_index(a, t));
+            sp_hi[t] = s.hi; sp_lo[t] = s.lo; sp_i[t] = (u32)s.cnt;
         }
     }
     __syncthreads();
     u64 i0, i1;
     ss_range(a, i0, i1);
-    for (u64 i = i0 + threadIdx.x; i < i1; i += SS_NT) {
+    for (u64 i = i0 + threadIdx.x; i < i1; i += NT) {
         const Rec r = a.rec[i];
-        u32 b;
-        if (SMALL) {
-            u32 l = 0, hh = a.B - 1;
-            while (l < hh) {
-                const u32 mid = (l + hh) >> 1;
-                if (!key3_lt(r.hi, r.lo, (u32)i, sp_hi[mid], sp_lo[mid], sp_i[mid])) l = mid + 1; else hh = mid;
-            }
-            b = l;
-        } else {
-            b = ss_bucket(a, r.hi, r.lo, (u32)i);
-        }
+        const u32 b = ss_find<SMALL>(a, r.hi, r.lo, (u32)i, sp_hi, sp_lo, sp_i);
         a.bid[i] = b;
         atomicAdd(&h[b], 1u);
     }
     __syncthreads();
-    for (u32 b = threadIdx.x; b < a.B; b += SS_NT) a.hist[(u64)b * a.G + blockIdx.x] = h[b];
+    for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + blockIdx.x] = h[b];
 }
 
 // the sample of a small sort (S <= TS_TILE): gathered and sorted in one workgroup's LDS,
@@ -398,19 +432,8 @@ __global__ __launch_bounds__(TS_NT) void k_ss_sample_sort(SortArgs a, Rec* smp) 
         si[j] = (uint16_t)j;
     }
     __syncthreads();
-    for (u32 k = 2; k <= P; k <<= 1)
-        for (u32 j = k >> 1; j > 0; j >>= 1) {
-            for (u32 t = tid; t < P / 2; t += TS_NT) {
-                const u32 i = 2 * t - (t & (j - 1)), p = i + j;
-                const u64 ah = sh[i], al = sl[i], bh = sh[p], bl = sl[p];
-                const uint16_t ai = si[i], bi = si[p];
-                if (key3_lt(bh, bl, bi, ah, al, ai) == ((i & k) == 0)) {
-                    sh[i] = bh; sl[i] = bl; sh[p] = ah; sl[p] = al;
-                    si[i] = bi; si[p] = ai;
-                }
-            }
-            __syncthreads();
-        }
+    lds_bitonic<TS_NT>(sh, sl, si, P);
+    __syncthreads();
     for (u32 j = tid; j < a.S; j += TS_NT) {
         Rec s;
         s.hi = sh[j]; s.lo = sl[j]; s.cnt = (u64)si[j] * a.n / a.S; s.ref = 0;
@@ -418,142 +441,107 @@ __global__ __launch_bounds__(TS_NT) void k_ss_sample_sort(SortArgs a, Rec* smp) 
     }
 }
 
-// items of workgroup g go to [hist[b][g], ...) of their bucket; the order inside a bucket does
-// not matter (the bucket sort orders by (hi, lo, index) completely)
+// records of workgroup g go to [hist[b][g], ...) of their bucket, whole (the bucket sort then
+// reads its records from one small region instead of gathering them from the whole array); the
+// order inside a bucket does not matter
 template <bool SMALL>
-__global__ __launch_bounds__(SS_NT) void k_ss_scatter(SortArgs a) {
+__global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_scatter(SortArgs a) {
+    constexpr int NT = SMALL ? SS_NT : SSL_NT;
     __shared__ u32 cur[SMALL ? SS_LDSB : SS_MAXB];
-    for (u32 b = threadIdx.x; b < a.B; b += SS_NT) cur[b] = a.hist[(u64)b * a.G + blockIdx.x];
+    for (u32 b = threadIdx.x; b < a.B; b += NT) cur[b] = a.hist[(u64)b * a.G + blockIdx.x];
     __syncthreads();
     u64 i0, i1;
     ss_range(a, i0, i1);
-    for (u64 i = i0 + threadIdx.x; i < i1; i += SS_NT) {
-        const Rec r = a.rec[i];
+    for (u64 i = i0 + threadIdx.x; i < i1; i += NT) {
         const u32 d = atomicAdd(&cur[a.bid[i]], 1u);
-        a.ikey[d] = make_uint4((u32)r.lo, (u32)(r.lo >> 32), (u32)r.hi, (u32)(r.hi >> 32));
-        a.iidx[d] = (u32)i;
+        a.irec[d] = a.rec[i];
     }
 }
 
-__device__ __forceinline__ u64 ik_hi(uint4 k) { return (u64)k.w << 32 | k.z; }
-__device__ __forceinline__ u64 ik_lo(uint4 k) { return (u64)k.y << 32 | k.x; }
+// load records X[0:cm) as (hi, lo, position) into LDS, padded to P entries
+__device__ __forceinline__ void sb_load(const Rec* X, u32 cm, u32 P, u64* kh, u64* kl, uint16_t* kp) {
+    for (u32 j = threadIdx.x; j < P; j += SB_NT) {
+        if (j < cm) { const Rec r = X[j]; kh[j] = r.hi; kl[j] = r.lo; }
+        else { kh[j] = ~0ull; kl[j] = ~0ull; }
+        kp[j] = (uint16_t)j;
+    }
+}
 
-// Oversized bucket (more than SS_CAP records: only when sampling was unlucky, or SS_TARGET was
-// forced up for a test): the workgroup sorts [s, s + m) of the item arrays through global
-// memory - LDS-sorted chunks of SS_CAP, then pairwise merge passes (ping-pong with ikey2/iidx2),
-// each pass split over the threads by merge-path partitions.  Returns the array holding the
-// result (0: ikey/iidx, 1: ikey2/iidx2).
-__device__ int ss_global_sort(const SortArgs& a, u64 s, u64 m, u64* sk_hi, u64* sk_lo, u32* sk_i) {
+// Oversized bucket (more than SB_CAP records: rare with SS_OVS samples per bucket, or forced by
+// WCG_SORT_TARGET in the tests): LDS-sorted chunks of SB_CAP, then pairwise merge passes between
+// irec and irec2 (thread t writes outputs [t * L / SB_NT, (t + 1) * L / SB_NT) of each pair,
+// split by merge path; A first on equal prefixes).  Equal prefixes (long keys) end up in any
+// order: the tie sort orders them afterwards.
+__device__ void ss_global_sort(const SortArgs& a, u64 s, u64 m, u64* kh, u64* kl, uint16_t* kp) {
     const int tid = threadIdx.x;
-    for (u64 c0 = 0; c0 < m; c0 += SS_CAP) {         // LDS bitonic per chunk
-        const u32 cm = (u32)(m - c0 < SS_CAP ? m - c0 : SS_CAP);
-        for (u32 e = tid; e < SS_CAP; e += SB_NT) {
-            if (e < cm) {
-                const uint4 k = a.ikey[s + c0 + e];
-                sk_hi[e] = ik_hi(k); sk_lo[e] = ik_lo(k); sk_i[e] = a.iidx[s + c0 + e];
-            } else { sk_hi[e] = ~0ull; sk_lo[e] = ~0ull; sk_i[e] = ~0u; }
-        }
+    Rec* X = a.irec + s;
+    Rec* Y = a.irec2 + s;
+    for (u64 c0 = 0; c0 < m; c0 += SB_CAP) {
+        const u32 cm = (u32)(m - c0 < SB_CAP ? m - c0 : SB_CAP);
+        sb_load(X + c0, cm, SB_CAP, kh, kl, kp);
         __syncthreads();
-        for (u32 k = 2; k <= SS_CAP; k <<= 1)
-            for (u32 j = k >> 1; j > 0; j >>= 1) {
-                for (u32 t = tid; t < SS_CAP / 2; t += SB_NT) {
-                    const u32 i = 2 * t - (t & (j - 1)), p = i + j;
-                    if (key3_lt(sk_hi[p], sk_lo[p], sk_i[p], sk_hi[i], sk_lo[i], sk_i[i]) == ((i & k) == 0)) {
-                        u64 x = sk_hi[i]; sk_hi[i] = sk_hi[p]; sk_hi[p] = x;
-                        x = sk_lo[i]; sk_lo[i] = sk_lo[p]; sk_lo[p] = x;
-                        const u32 y = sk_i[i]; sk_i[i] = sk_i[p]; sk_i[p] = y;
-                    }
-                }
-                __syncthreads();
-            }
-        for (u32 e = tid; e < cm; e += SB_NT) {
-            a.ikey[s + c0 + e] = make_uint4((u32)sk_lo[e], (u32)(sk_lo[e] >> 32), (u32)sk_hi[e], (u32)(sk_hi[e] >> 32));
-            a.iidx[s + c0 + e] = sk_i[e];
-        }
+        lds_bitonic<SB_NT>(kh, kl, kp, SB_CAP);
+        __syncthreads();
+        for (u32 e = tid; e < cm; e += SB_NT) Y[c0 + e] = X[c0 + kp[e]];
         __syncthreads();
     }
-    int src = 0;
-    for (u64 w = SS_CAP; w < m; w *= 2) {
-        const uint4* KI = src ? a.ikey2 : a.ikey;
-        const u32* II = src ? a.iidx2 : a.iidx;
-        uint4* KO = src ? a.ikey : a.ikey2;
-        u32* IO = src ? a.iidx : a.iidx2;
+    const Rec* src = Y;
+    Rec* dst = X;
+    for (u64 w = SB_CAP; w < m; w *= 2) {
         for (u64 p0 = 0; p0 < m; p0 += 2 * w) {
             const u64 la = m - p0 < w ? m - p0 : w;
             const u64 lb = m - p0 - la < w ? m - p0 - la : w;
             const u64 L = la + lb;
-            const u64 A = s + p0, Bq = s + p0 + la;
-            // thread t writes outputs [t * L / SB_NT, (t + 1) * L / SB_NT)
+            const Rec* A = src + p0;
+            const Rec* Bq = A + la;
             const u64 d0 = L * tid / SB_NT, d1 = L * (tid + 1) / SB_NT;
-            auto lt_at = [&](u64 x, u64 y) -> bool {       // item x (in B) < item y (in A)?
-                const uint4 kx = KI[x], ky = KI[y];
-                return key3_lt(ik_hi(kx), ik_lo(kx), II[x], ik_hi(ky), ik_lo(ky), II[y]);
-            };
             u64 lo = d0 > lb ? d0 - lb : 0, hi = d0 < la ? d0 : la;   // #A among the first d0
             while (lo < hi) {
                 const u64 mid = (lo + hi) >> 1;
-                if (lt_at(Bq + (d0 - 1 - mid), A + mid)) hi = mid; else lo = mid + 1;
+                const Rec& x = Bq[d0 - 1 - mid];
+                const Rec& y = A[mid];
+                if (pre_lt(x.hi, x.lo, y.hi, y.lo)) hi = mid; else lo = mid + 1;
             }
             u64 ia = lo, ib = d0 - lo;
             for (u64 d = d0; d < d1; d++) {
                 bool takeA;
                 if (ia >= la) takeA = false;
                 else if (ib >= lb) takeA = true;
-                else takeA = !lt_at(Bq + ib, A + ia);
-                const u64 q = takeA ? A + ia : Bq + ib;
-                KO[s + p0 + d] = KI[q];
-                IO[s + p0 + d] = II[q];
-                if (takeA) ia++; else ib++;
+                else takeA = !pre_lt(Bq[ib].hi, Bq[ib].lo, A[ia].hi, A[ia].lo);
+                dst[p0 + d] = takeA ? A[ia++] : Bq[ib++];
             }
         }
         __syncthreads();
-        src ^= 1;
+        const Rec* t = src; src = dst; dst = const_cast<Rec*>(t);
     }
-    return src;
+    for (u64 j = tid; j < m; j += SB_NT) a.out[s + j] = src[j];
 }
 
-// one workgroup per bucket: bitonic sort of (hi, lo, index) in LDS, then gather the records
+// one workgroup per bucket: bitonic sort of (hi, lo, position) in LDS, then the records are
+// permuted from the bucket's region (L2-resident) into place
 __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
-    __shared__ u64 sk_hi[SS_CAP], sk_lo[SS_CAP];
-    __shared__ u32 sk_i[SS_CAP];
+    __shared__ u64 kh[SB_CAP], kl[SB_CAP];
+    __shared__ uint16_t kp[SB_CAP];
     const u32 b = blockIdx.x;
     const u64 s = a.hist[(u64)b * a.G];
     const u64 e = b + 1 < a.B ? a.hist[(u64)(b + 1) * a.G] : a.n;
     const u64 m = e - s;
-    const int tid = threadIdx.x;
     if (m == 0) return;
-    if (m > SS_CAP) {
-        const int src = ss_global_sort(a, s, m, sk_hi, sk_lo, sk_i);
-        const u32* II = src ? a.iidx2 : a.iidx;
-        for (u64 j = tid; j < m; j += SB_NT) a.out[s + j] = a.rec[II[s + j]];
-        return;
-    }
+    if (m > SB_CAP) { ss_global_sort(a, s, m, kh, kl, kp); return; }
     u32 P = 64;
     while (P < m) P <<= 1;
-    for (u32 j = tid; j < P; j += SB_NT) {
-        if (j < m) {
-            const uint4 k = a.ikey[s + j];
-            sk_hi[j] = ik_hi(k); sk_lo[j] = ik_lo(k); sk_i[j] = a.iidx[s + j];
-        } else { sk_hi[j] = ~0ull; sk_lo[j] = ~0ull; sk_i[j] = ~0u; }
-    }
+    const Rec* X = a.irec + s;
+    sb_load(X, (u32)m, P, kh, kl, kp);
     __syncthreads();
-    for (u32 k = 2; k <= P; k <<= 1)
-        for (u32 j = k >> 1; j > 0; j >>= 1) {
-            for (u32 t = tid; t < P / 2; t += SB_NT) {
-                const u32 i = 2 * t - (t & (j - 1)), p = i + j;
-                const u64 ah = sk_hi[i], al = sk_lo[i], bh = sk_hi[p], bl = sk_lo[p];
-                const u32 ai = sk_i[i], bi = sk_i[p];
-                if (key3_lt(bh, bl, bi, ah, al, ai) == ((i & k) == 0)) {
-                    sk_hi[i] = bh; sk_lo[i] = bl; sk_i[i] = bi;
-                    sk_hi[p] = ah; sk_lo[p] = al; sk_i[p] = ai;
-                }
-            }
-            __syncthreads();
-        }
-    for (u32 j = tid; j < m; j += SB_NT) a.out[s + j] = a.rec[sk_i[j]];
+    lds_bitonic<SB_NT>(kh, kl, kp, P);
+    __syncthreads();
+    for (u32 j = threadIdx.x; j < m; j += SB_NT) a.out[s + j] = X[kp[j]];
 }
 
 // ---------------------------------------------------------------- tie groups
+__device__ __forceinline__ u64 ik_hi(uint4 k) { return (u64)k.w << 32 | k.z; }
+__device__ __forceinline__ u64 ik_lo(uint4 k) { return (u64)k.y << 32 | k.x; }
+
 // A record's key bytes: inline keys are their prefix; a long key (ref & LONG_FLAG) lives at
 // base + (ref & LONG_OFF_MASK), (ref >> 40) & LONG_LEN_MAX bytes - base is the long-key arena
 // (zero-padded 16-byte cells) or, for merged runs, the formatted text (any alignment).

@@ -223,3 +223,27 @@ def test_full_size_c2(built):
     r = ob.Result(data, 16)
     ob.assert_same(got, r.merged())
     assert st["tokens"] == r.ntokens and nk == r.nkeys
+
+
+@pytest.mark.parametrize("shape", ["mixed_16_50", "exactly_16", "runs_100_300"])
+def test_long_token_lengths(built, shape):
+    """Inputs made only of long tokens (every step logs dozens): each logged length must be the
+    token's (a spilled prefetch register once gave whole steps stale letter masks, so lengths of
+    1-5 bytes), repeats fold in k_long_hash's cache, partitions aggregate in k_long_agg."""
+    import wcg
+    rng = random.Random({"mixed_16_50": 1, "exactly_16": 2, "runs_100_300": 3}[shape])
+    if shape == "mixed_16_50":
+        words = [bytes(rng.choice(b"abcdefgh") for _ in range(rng.randrange(16, 50))) for _ in range(3000)]
+        data = b" ".join(rng.choice(words) for _ in range(100_000)) + b"\n"
+    elif shape == "exactly_16":
+        words = [bytes(rng.choice(b"abcdefgh") for _ in range(16)) for _ in range(3000)]
+        data = b" ".join(rng.choice(words) for _ in range(100_000)) + b" " + b" ".join(words) + b"\n"
+    else:                                   # runs past the 1 KiB window: walked by k_long_hash
+        words = [bytes(rng.choice(b"abcdefgh") for _ in range(rng.randrange(100, 300))) for _ in range(300)]
+        data = b" ".join(rng.choice(words) for _ in range(20_000)) + b"\n"
+    with wcg.Engine(0, 0, 1 << 20) as e:
+        e.reset()
+        e.map_host(data)
+        e.reduce()
+        ob.assert_same(e.result(), ob.merged(data))
+        assert e.stats()["overflow"] == 0
