@@ -89,10 +89,24 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
 }
 
 // ---------------------------------------------------------------- formatting
+// decimal digits of a count: compares against powers of ten (a u64 division is a long software
+// routine on the GPU)
 __device__ __forceinline__ u32 ndigits(u64 v) {
     u32 d = 1;
-    while (v >= 10) { v /= 10; d++; }
+    u64 p = 10;
+#pragma unroll
+    for (int k = 1; k < 20; k++) { d += v >= p ? 1u : 0u; p *= 10; }
     return d;
+}
+// the nd decimal digits of v at o[0..nd) (32-bit divisions by 10 are multiplies)
+template <typename P>
+__device__ __forceinline__ void put_digits(P o, u64 v, u32 nd) {
+    if (v < (1ull << 32)) {
+        u32 c = (u32)v;
+        for (int k = (int)nd - 1; k >= 0; k--) { o[k] = (uint8_t)('0' + c % 10u); c /= 10u; }
+    } else {
+        for (int k = (int)nd - 1; k >= 0; k--) { o[k] = (uint8_t)('0' + v % 10); v /= 10; }
+    }
 }
 __device__ __forceinline__ u64 rec_len(const Rec& r) { return (r.ref & LONG_FLAG) ? ((r.ref >> 40) & LONG_LEN_MAX) : r.ref; }
 __device__ __forceinline__ u32 rec_byte(const Rec& r, u64 k, const uint8_t* arena) {
@@ -154,17 +168,9 @@ __global__ __launch_bounds__(FM_NT) void k_fmt_sum(const Rec* r, u64 n, int fmt,
     if (threadIdx.x == 0) tsum[blockIdx.x] = all;
 }
 
-__global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, int fmt, u32 nreduce, u32 part,
-                                                    const uint8_t* arena, const u64* toff, uint8_t* out) {
-    __shared__ u64 ws[FM_NT / 64];
-    const u64 i0 = (u64)blockIdx.x * FM_TILE + (u64)threadIdx.x * FM_IPT;
-    u64 L[FM_IPT], s = 0;
-    for (int k = 0; k < FM_IPT; k++) {
-        L[k] = i0 + k < n ? line_len(r[i0 + k], fmt, nreduce, part, arena) : 0;
-        s += L[k];
-    }
-    u64 all;
-    uint8_t* o = out + toff[blockIdx.x] + block_excl_scan(s, ws, all);
+// the lines of records r[i0, i0 + FM_IPT) with lengths L[] at o (global memory or LDS)
+template <typename P>
+__device__ __forceinline__ void fmt_lines(const Rec* r, u64 i0, const u64* L, int fmt, const uint8_t* arena, P o) {
     for (int q = 0; q < FM_IPT; q++) {
         if (L[q] == 0) continue;
         const Rec x = r[i0 + q];
@@ -180,7 +186,13 @@ __global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, int fm
             const char* pre = "{\"Key\":\"";
             for (int k = 0; k < 8; k++) *o++ = pre[k];
         }
-        for (u64 k = 0; k < len; k++) *o++ = (uint8_t)rec_byte(x, k, arena);
+        if (x.ref & LONG_FLAG) {
+            const uint8_t* src = arena + (x.ref & LONG_OFF_MASK);
+            for (u64 k = 0; k < len; k++) *o++ = src[k];
+        } else {
+            for (u64 k = 0; k < len; k++)
+                *o++ = (uint8_t)(k < 8 ? x.hi >> (56 - 8 * k) : x.lo >> (56 - 8 * (k - 8)));
+        }
         if (json) {
             const char* mid = "\",\"Value\":\"";
             for (int k = 0; k < 11; k++) *o++ = mid[k];
@@ -188,11 +200,43 @@ __global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, int fm
             *o++ = ':'; *o++ = ' ';
         }
         const u32 nd = ndigits(x.cnt);
-        u64 c = x.cnt;
-        for (int k = (int)nd - 1; k >= 0; k--) { o[k] = (uint8_t)('0' + c % 10); c /= 10; }
+        put_digits(o, x.cnt, nd);
         o += nd;
         if (json) { *o++ = '"'; *o++ = '}'; }
         *o++ = '\n';
+    }
+}
+
+// A tile's lines are formatted into LDS (byte stores there are cheap) and leave in aligned
+// 16-byte stores; the destination's alignment is kept by offsetting the LDS image by
+// (dst & 15).  A tile larger than the stage (long keys) writes its bytes directly.
+constexpr u32 FM_STAGE = 32768;
+__global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, int fmt, u32 nreduce, u32 part,
+                                                    const uint8_t* arena, const u64* toff, uint8_t* out) {
+    __shared__ u64 ws[FM_NT / 64];
+    __shared__ __align__(16) uint8_t sb[FM_STAGE];
+    const u64 i0 = (u64)blockIdx.x * FM_TILE + (u64)threadIdx.x * FM_IPT;
+    u64 L[FM_IPT], s = 0;
+    for (int k = 0; k < FM_IPT; k++) {
+        L[k] = i0 + k < n ? line_len(r[i0 + k], fmt, nreduce, part, arena) : 0;
+        s += L[k];
+    }
+    u64 all;
+    const u64 lo = block_excl_scan(s, ws, all);
+    uint8_t* const dst = out + toff[blockIdx.x];
+    const u32 pad = (u32)((uintptr_t)dst & 15);
+    if (pad + all > FM_STAGE) {                     // workgroup-uniform
+        fmt_lines(r, i0, L, fmt, arena, dst + lo);
+        return;
+    }
+    fmt_lines(r, i0, L, fmt, arena, sb + pad + lo);
+    __syncthreads();
+    uint8_t* const base = dst - pad;                // 16-byte aligned; sb[b] is base[b]
+    const u32 total = pad + (u32)all;
+    for (u32 c = threadIdx.x; 16 * c < total; c += FM_NT) {
+        const u32 b0 = 16 * c, b1 = b0 + 16 < total ? b0 + 16 : total;
+        if (b0 >= pad && b1 == b0 + 16) *reinterpret_cast<uint4*>(base + b0) = *reinterpret_cast<const uint4*>(sb + b0);
+        else for (u32 b = b0 > pad ? b0 : pad; b < b1; b++) base[b] = sb[b];
     }
 }
 
