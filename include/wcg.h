@@ -167,10 +167,10 @@ WCG_API int wcg_timings(wcg_ctx *ctx, double *ms, int n, uint64_t *map_launches)
 /* Enable/disable the event timing above (off by default: it adds event records). */
 WCG_API int wcg_enable_timing(wcg_ctx *ctx, int on);
 
-/* Diagnostics, stats8 = {tokens, distinct keys, tokens counted in LDS, global-table operations,
+/* Diagnostics, stats9 = {tokens, distinct keys, tokens counted in LDS, global-table operations,
  * tokens > 15 bytes, long-key heap bytes (keys > 32 bytes; shorter long keys live in their
- * table slot's cell), overflow, spin_fail}. */
-WCG_API int wcg_stats(wcg_ctx *ctx, uint64_t *stats8);
+ * table slot's cell), overflow, spin_fail, records emitted by the second aggregation pass}. */
+WCG_API int wcg_stats(wcg_ctx *ctx, uint64_t *stats9);
 
 /* FNV-1a 32 (= ihash, mapreduce.go:185-189), host side, for partition arithmetic. */
 WCG_API uint32_t wcg_ihash(const uint8_t *key, uint64_t len);

@@ -1,11 +1,25 @@
-// wcg_agg.h - second aggregation stage: the miss log of k_map, one hash bucket at a time.
+// wcg_agg.h - aggregation of k_map's miss log, one hash bucket at a time, in two passes.
 //
 // k_map leaves, per (workgroup w, bucket p), a region of miss-log units (wcg_lds_table.h): keys that missed
 // w's LDS table plus w's flushed LDS slots (with counts).  Every key of bucket p lands only in
 // bucket-p regions, so a workgroup that aggregates bucket p over a slice of source regions
 // needs LDS for (distinct keys of p) / 1 - about 1/P of the vocabulary - and flushes each
 // distinct key once: the per-token global atomics of a naive design become per-(slice, key)
-// atomics.  Overflow of the LDS table still falls back to the global table (exact, slower).
+// atomics.
+//
+// Pass 1 (k_agg, mode AGG_SPILL): workgroup (p, s) aggregates bucket p over slice s; its LDS table
+// is flushed to the global table.  An entry the full table cannot take is appended, whole, to
+// the workgroup's spill region (an LDS cursor: no global atomic).  Low-cardinality text (C2) never
+// spills.  High-cardinality text (C4: 22M distinct inline keys per GiB, 347K per bucket against
+// 6,760 LDS slots) spills nearly everything, and per-occurrence global inserts of the spilled
+// entries were 5.8 of a 19 ms step.
+// k_rp: each pass-1 workgroup's spill is split by 7 more hash bits into AGG_Q sub-buckets (LDS
+// staging, whole entries), so a sub-bucket holds ~1/8192 of the keys.
+// Pass 2 (k_agg, mode AGG_EMIT): one workgroup per (p, q) sub-bucket aggregates it in LDS and emits
+// each distinct key as a record straight into the record log (no global-table insert); the
+// sub-buckets are disjoint, and keys also counted in the global table (pass-1 flushes) or emitted
+// by another map call are merged after the sort (wcg_sort.h: k_dd_*).  A full LDS table or a full
+// record log falls back to global-table inserts (exact either way).
 #pragma once
 #include "wcg_common.h"
 #include "wcg_lds_table.h"
@@ -15,128 +29,250 @@ namespace wcg {
 constexpr int AGG_NT = 1024;
 constexpr u32 AGG_BATCH = AGG_NT * 4;     // units per batch (4 per thread)
 constexpr int AGG_W = 2;               // ways per bucket (16-byte k0 rows: wcg_lds_table.h)
-constexpr int AGG_NB = 3380;           // 3380 x 2 slots x 24 B (u64 counts) = 162240 B (+ 1.5 KiB)
+constexpr int AGG_NB = 3350;           // 3350 x 2 slots x 24 B (u64 counts) = 160800 B (+ 2.5 KiB)
 constexpr u32 AGG_SLACK_UNITS = AGG_BATCH + 8;   // pool tail slack for k_agg's unmasked loads
 constexpr u32 AGG_MAX_SRC = 256;       // source regions per workgroup (+1 KiB LDS = 160 KiB)
+constexpr u32 AGG_Q = 128;             // pass-2 sub-buckets per bucket
+constexpr int AGG_SPILL = 0, AGG_EMIT = 1;
 
 struct AggArgs {
+    // sources: bucket b's regions are pool + ((wbase + k * wstep) * rstride + b % rmod) * region_cap
+    // for k in [k0, k1) (pass 1: every map workgroup in a slice; pass 2: the pass-1 workgroups of
+    // the sub-bucket's bucket), region_len indexed like the regions
     const u64* pool;
     const u32* region_len;
     u64 region_cap;
-    u32 P;                 // miss buckets
-    u32 nsrc;              // source workgroups of k_map
-    u32 slices;            // workgroups per bucket
+    u32 P;                 // pass 1: miss buckets; pass 2: buckets x AGG_Q sub-buckets
+    u32 nsrc;              // pass 1: source workgroups of k_map; pass 2: pass-1 slices
+    u32 slices;            // workgroups per bucket (pass 2: 1)
+    u32 rstride, rmod;     // region index = w * rstride + b % rmod
+    u32 P1;                // pass 2: pass-1 buckets (source w of sub-bucket b: b / AGG_Q + P1 * s)
+    int mode;              // AGG_SPILL (pass 1) or AGG_EMIT (pass 2)
     GEntry* gtab;
     u64 gmask;
     DevState* st;
-    const u64* map_stats;  // k_map's per-workgroup stats [nsrc][4], summed by workgroup 0
+    const u64* map_stats;  // k_map's per-workgroup stats [nsrc][4], summed by workgroup 0 (pass 1)
+    u64* spill;            // pass 1: spill region of workgroup b = spill + b * spill_cap
+    u64 spill_cap;
+    u32* spill_len;
+    Rec* emit;             // pass 2: record log (emit_cap records; st->nemit used)
+    u64 emit_cap;
 };
 
-__global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
-    __shared__ __align__(16) u64 tk0[AGG_NB][AGG_W];
-    __shared__ __align__(16) u64 tk1[AGG_NB][AGG_W];
-    __shared__ u64 tcnt[AGG_NB][AGG_W];
-    __shared__ u32 rlen_s[AGG_MAX_SRC];
+// the record of an inline key (k0, k1) of fact F4 (the same conversion as k_compact's)
+__device__ __forceinline__ Rec inline_rec(u64 k0, u64 k1, u64 cnt) {
+    Rec r;
+    if (key_short(k0)) {
+        r.hi = bswap64(k0 & 0x00FFFFFFFFFFFFFFull);
+        r.lo = 0;
+        r.ref = k0 >> 56;
+    } else {
+        r.hi = bswap64(k0);
+        r.lo = bswap64(k1 & 0x00FFFFFFFFFFFFFFull);
+        r.ref = k1 >> 56;
+    }
+    r.cnt = cnt;
+    return r;
+}
+
+// decode the entries headed by 4 of a lane's units (u[0..6): its 4 units and the 2 after them;
+// units past the region are 0 = filler)
+__device__ __forceinline__ void agg_decode(const u64 (&u)[6], u64 (&k0)[4], u64 (&k1)[4], u64 (&c)[4], bool (&v)[4],
+                                           u32 (&nu)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const u32 T = (u32)(u[k] >> 56);
+        const bool head = T >= 0x41;
+        v[k] = T != 0 && (head || (T & 0x1F) < 8);   // skip counts, fillers, medium tails
+        const u64 last = head ? u[k + 1] : u[k];     // unit carrying the count flag
+        k0[k] = head ? u[k] : (u[k] & ~U_CNT);
+        k1[k] = head ? (u[k + 1] & ~U_CNT) : 0;
+        const bool hc = (last & U_CNT) != 0;
+        c[k] = hc ? (head ? u[k + 2] : u[k + 1]) : 1;
+        nu[k] = (head ? 2u : 1u) + (hc ? 1u : 0u);
+    }
+}
+
+// One (bucket, slice) of k_agg: index bi = p + P * s.  Returns the global-table inserts made.
+__device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[AGG_W], u64 (*tcnt)[AGG_W], u32* rlen_s,
+                       u32* bstart, u32& spos, u64 (*wsum)[4]) {
     const int tid = threadIdx.x;
     LdsTable<AGG_NB, u64, AGG_W> tab{tk0, tk1, tcnt};
+    const bool emit = a.mode == AGG_EMIT;
+    const u32 p = bi % a.P, s = bi / a.P;
+    u32 k0_, k1_, wbase, wstep;
+    if (!emit) {
+        k0_ = (u32)(((u64)a.nsrc * s) / a.slices); k1_ = (u32)(((u64)a.nsrc * (s + 1)) / a.slices);
+        wbase = 0; wstep = 1;
+    } else {
+        k0_ = 0; k1_ = a.nsrc;
+        wbase = p / AGG_Q; wstep = a.P1;
+    }
+    const u32 nk = k1_ - k0_;
+    auto region = [&](u32 k) -> u64 { return (u64)(wbase + k * wstep) * a.rstride + p % a.rmod; };
+    constexpr u32 WB = 256;                          // units per wave batch
+    // region lengths and the running count of batches before each region, staged once: a global
+    // load in the batch walk would be a vmcnt wait that drains the prefetch
+    for (u32 k = tid; k < nk; k += AGG_NT) rlen_s[k] = a.region_len[region(k0_ + k)];
+    __syncthreads();
+    if (tid == 0) {
+        u32 t = 0;
+        for (u32 k = 0; k < nk; k++) { bstart[k] = t; t += (rlen_s[k] + WB - 1) / WB; }
+        bstart[nk] = t;
+        spos = 0;
+    }
+    __syncthreads();
+    const u32 nbat = bstart[nk];
+    if (nbat == 0) {                                  // nothing to read (pass 2 on low-cardinality
+        if (!emit && tid == 0) a.spill_len[bi] = 0;   // text: every sub-bucket empty): done before
+        return 0;                                     // the table's 162 KiB are initialised
+    }
     tab.init(tid, AGG_NT);
-    const u32 p = blockIdx.x % a.P, s = blockIdx.x / a.P;
-    const u32 w0 = (u32)(((u64)a.nsrc * s) / a.slices), w1 = (u32)(((u64)a.nsrc * (s + 1)) / a.slices);
-    // region lengths of this slice, staged once: a global load in the batch walk would be a
-    // vmcnt wait that drains the prefetch
-    for (u32 w = w0 + tid; w < w1; w += AGG_NT) rlen_s[w - w0] = a.region_len[(u64)w * a.P + p];
     __syncthreads();
     u64 my_global = 0;
-    // Every wave walks its own regions (w0 + wave, + 16, ...) in wave batches of 256 units:
-    // lane l takes units [4l, 4l + 4) and also loads the two after them, so a medium-key head or
-    // a count flag finds its neighbours in registers (units past the region's length are masked
-    // to 0 = filler).  The next wave batch is loaded into the other register set while this one
-    // is aggregated, and no barrier ties the waves together, so 16 waves x 2 batches are in
-    // flight per CU: a workgroup-wide batch walk kept only 2, and k_agg ran at the HBM latency
-    // of one batch per region even for nearly empty regions.
-    const int wave = tid >> 6, lane = tid & 63;
-    constexpr u32 WB = 256;                          // units per wave batch
-    constexpr u32 WSTRIDE = AGG_NT / 64;             // regions between a wave's regions
-    auto rlen = [&](u32 w) -> u32 { return rlen_s[w - w0]; };
-    auto next_batch = [&](u32& w, u32& b) {          // wave-uniform walk over non-empty batches
-        b++;
-        while (w < w1 && (u64)b * WB >= rlen(w)) { w += WSTRIDE; b = 0; }
+    u64* const sp = emit ? nullptr : a.spill + (u64)bi * a.spill_cap;
+    // count c of (k0, k1) the table could not take: pass 1 spills the entry, pass 2 (and a full
+    // spill region) inserts it into the global table
+    auto overflow = [&](u64 k0, u64 k1, u64 c, u32 nu) {
+        if (!emit) {
+            const u32 pos = atomicAdd(&spos, nu);
+            if (pos + nu <= a.spill_cap) {
+                u64 e[3];
+                const u64 f = c > 1 ? U_CNT : 0;
+                if (key_short(k0)) { e[0] = k0 | f; e[1] = c; }
+                else { e[0] = k0; e[1] = k1 | f; e[2] = c; }
+                for (u32 j = 0; j < nu; j++) sp[pos + j] = e[j];
+                return;
+            }
+            for (u64 j = pos; j < a.spill_cap; j++) sp[j] = 0;   // reserved, inside: fillers
+        }
+        my_global++;
+        ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
     };
-    auto load = [&](u32 w, u32 b, v4u& x0, v4u& x1, v4u& x2) {
-        const bool live = w < w1;
-        const u32 i = b * WB + 4 * lane, lim = live ? rlen(w) : 0;
-        const v4u* q = reinterpret_cast<const v4u*>(a.pool + ((u64)(live ? w : w0) * a.P + p) * a.region_cap + i);
-        (void)lim;                    // units past the region's length are masked in process()
+    // The workgroup's wave batches (256 units) are dealt round-robin over its 16 waves: lane l
+    // takes units [4l, 4l + 4) and also loads the two after them, so a medium-key head or a count
+    // flag finds its neighbours in registers (units past the region's length are masked to 0 =
+    // filler).  The next batch is loaded into the other register set while this one is
+    // aggregated, and no barrier ties the waves together, so 16 waves x 2 batches are in flight
+    // per CU (a workgroup-wide batch walk kept only 2, and ran at the HBM latency of one batch
+    // per region even for nearly empty regions; a region per wave left most waves idle when a
+    // workgroup has few regions, as in pass 2).
+    const int wave = tid >> 6, lane = tid & 63;
+    constexpr u32 WSTRIDE = AGG_NT / 64;
+    // (region k, batch b) of a wave's batch g, advanced incrementally: g grows by WSTRIDE per
+    // step, which crosses at most a few region ends
+    auto advance = [&](u32& k, u32& b, u32 step) {
+        b += step;
+        while (k < nk) {
+            const u32 nbk = bstart[k + 1] - bstart[k];
+            if (b < nbk) break;
+            b -= nbk;
+            k++;
+        }
+    };
+    auto load = [&](u32 k, u32 b, v4u& x0, v4u& x1, v4u& x2) {
+        const bool live = k < nk;
+        const u32 i = b * WB + 4 * lane;
+        const v4u* q = reinterpret_cast<const v4u*>(a.pool + region(k0_ + (live ? k : 0)) * a.region_cap + i);
         x0 = q[0];                    // unconditional (the pool has AGG_SLACK_UNITS of slack),
         x1 = q[1];                    // so no branch splits the loads from the waits that let
         x2 = q[2];                    // the next batch stay in flight
     };
     auto unit = [](const v4u& x, int h) -> u64 { return h ? ((u64)x.w << 32 | x.z) : ((u64)x.y << 32 | x.x); };
-    auto process = [&](u32 w, u32 b, const v4u& x0, const v4u& x1, const v4u& x2) {
+    auto process = [&](u32 k, u32 b, const v4u& x0, const v4u& x1, const v4u& x2) {
         u64 u[6] = {unit(x0, 0), unit(x0, 1), unit(x1, 0), unit(x1, 1), unit(x2, 0), unit(x2, 1)};
-        const u32 i0 = b * WB + 4 * lane, len = rlen(w);
+        const u32 i0 = b * WB + 4 * lane, len = rlen_s[k];
 #pragma unroll
-        for (int k = 0; k < 6; k++) u[k] = i0 + k < len ? u[k] : 0;
+        for (int j = 0; j < 6; j++) u[j] = i0 + j < len ? u[j] : 0;
         u64 k0[4], k1[4], c[4];
         bool v[4];
+        u32 nu[4];
+        agg_decode(u, k0, k1, c, v, nu);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const u32 T = (u32)(u[k] >> 56);
-            const bool head = T >= 0x41;
-            v[k] = T != 0 && (head || (T & 0x1F) < 8);   // skip counts, fillers, medium tails
-            const u64 last = head ? u[k + 1] : u[k];     // unit carrying the count flag
-            k0[k] = head ? u[k] : (u[k] & ~U_CNT);
-            k1[k] = head ? (u[k + 1] & ~U_CNT) : 0;
-            c[k] = (last & U_CNT) ? (head ? u[k + 2] : u[k + 1]) : 1;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k += 2) {
+        for (int j = 0; j < 4; j += 2) {
             typename decltype(tab)::Probe pa, pb;
-            if (v[k]) tab.start(lds_hash(k0[k], k1[k]), pa);
-            if (v[k + 1]) tab.start(lds_hash(k0[k + 1], k1[k + 1]), pb);
-            if (v[k] && !tab.finish(k0[k], k1[k], pa, c[k])) {
-                my_global++;
-                ginsert(a.gtab, a.gmask, k0[k], k1[k], gslot(key_hash(k0[k], k1[k])), c[k], a.st);
-            }
-            if (v[k + 1] && !tab.finish(k0[k + 1], k1[k + 1], pb, c[k + 1])) {
-                my_global++;
-                ginsert(a.gtab, a.gmask, k0[k + 1], k1[k + 1], gslot(key_hash(k0[k + 1], k1[k + 1])), c[k + 1], a.st);
-            }
+            if (v[j]) tab.start(lds_hash(k0[j], k1[j]), pa);
+            if (v[j + 1]) tab.start(lds_hash(k0[j + 1], k1[j + 1]), pb);
+            if (v[j] && !tab.finish(k0[j], k1[j], pa, c[j])) overflow(k0[j], k1[j], c[j], nu[j]);
+            if (v[j + 1] && !tab.finish(k0[j + 1], k1[j + 1], pb, c[j + 1])) overflow(k0[j + 1], k1[j + 1], c[j + 1], nu[j + 1]);
         }
     };
-    u32 wa = w0 + wave, ba = (u32)-1;
-    next_batch(wa, ba);
-    u32 wb = wa, bb = ba;
-    next_batch(wb, bb);
+    u32 ka = 0, ba = 0;
+    advance(ka, ba, wave);
+    u32 kb = ka, bb = ba;
+    advance(kb, bb, WSTRIDE);
     v4u a0, a1, a2, b0, b1, b2;
-    load(wa, ba, a0, a1, a2);
-    load(wb, bb, b0, b1, b2);
-    while (wa < w1) {
-        process(wa, ba, a0, a1, a2);
-        u32 wn = wb, bn = bb;
-        next_batch(wn, bn);
-        wa = wn; ba = bn;
-        load(wa, ba, a0, a1, a2);
-        if (wb >= w1) break;
-        process(wb, bb, b0, b1, b2);
-        wn = wa; bn = ba;
-        next_batch(wn, bn);
-        wb = wn; bb = bn;
-        load(wb, bb, b0, b1, b2);
+    load(ka, ba, a0, a1, a2);
+    load(kb, bb, b0, b1, b2);
+    while (ka < nk) {
+        process(ka, ba, a0, a1, a2);
+        ka = kb; ba = bb;
+        advance(ka, ba, WSTRIDE);
+        load(ka, ba, a0, a1, a2);
+        if (kb >= nk) break;
+        process(kb, bb, b0, b1, b2);
+        kb = ka; bb = ba;
+        advance(kb, bb, WSTRIDE);
+        load(kb, bb, b0, b1, b2);
     }
     __syncthreads();
-    for (int i = tid; i < AGG_NB * AGG_W; i += AGG_NT) {
-        const u64 c = (&tcnt[0][0])[i];
-        if (!c) continue;
-        const u64 k0 = (&tk0[0][0])[i], k1 = (&tk1[0][0])[i];
-        my_global++;
-        ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
+    if (!emit && tid == 0) a.spill_len[bi] = spos < a.spill_cap ? spos : (u32)a.spill_cap;
+    if (!emit) {
+        for (int i = tid; i < AGG_NB * AGG_W; i += AGG_NT) {
+            const u64 c = (&tcnt[0][0])[i];
+            if (!c) continue;
+            const u64 k0 = (&tk0[0][0])[i], k1 = (&tk1[0][0])[i];
+            my_global++;
+            ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
+        }
+    } else {
+        // pass 2: this sub-bucket's keys, one record each, placed by one atomic per workgroup;
+        // positions past the log's end go to the global table instead (the log stays dense:
+        // k_copy_emit takes min(nemit, cap) records)
+        u32 mine = 0;
+        for (int i = tid; i < AGG_NB * AGG_W; i += AGG_NT) mine += (&tcnt[0][0])[i] ? 1u : 0u;
+        u32 incl = mine;
+        for (int d = 1; d < 64; d <<= 1) { const u32 y = __shfl_up(incl, d, 64); if (lane >= d) incl += y; }
+        if (lane == 63) wsum[wave][0] = incl;
+        __syncthreads();
+        u32 pre = 0, all = 0;
+        for (int w = 0; w < AGG_NT / 64; w++) { if (w < wave) pre += (u32)wsum[w][0]; all += (u32)wsum[w][0]; }
+        if (tid == 0) wsum[0][1] = all ? atomicAdd((unsigned long long*)&a.st->nemit, (unsigned long long)all) : 0;
+        __syncthreads();
+        u64 pos = wsum[0][1] + pre + incl - mine;
+        for (int i = tid; i < AGG_NB * AGG_W; i += AGG_NT) {
+            const u64 c = (&tcnt[0][0])[i];
+            if (!c) continue;
+            const u64 k0 = (&tk0[0][0])[i], k1 = (&tk1[0][0])[i];
+            if (pos < a.emit_cap) a.emit[pos] = inline_rec(k0, k1, c);
+            else { my_global++; ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st); }
+            pos++;
+        }
     }
+    __syncthreads();                                  // the LDS is reused by the next bucket
+    return my_global;
+}
+
+// pass 1: one workgroup per (bucket, slice); pass 2: a persistent grid over the sub-buckets (most
+// are empty on low-cardinality text, and an empty one costs a few LDS reads instead of a launch
+// of a 160 KiB workgroup)
+__global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
+    __shared__ __align__(16) u64 tk0[AGG_NB][AGG_W];
+    __shared__ __align__(16) u64 tk1[AGG_NB][AGG_W];
+    __shared__ u64 tcnt[AGG_NB][AGG_W];
+    __shared__ u32 rlen_s[AGG_MAX_SRC];
+    __shared__ u32 bstart[AGG_MAX_SRC + 1];
+    __shared__ u32 spos;                       // pass 1: spill cursor
+    __shared__ u64 wsum[AGG_NT / 64][4];       // per-wave sums (the record log's counts, stats)
+    const int tid = threadIdx.x;
+    const u32 nb = a.P * a.slices;
+    u64 my_global = 0;
+    for (u32 bi = blockIdx.x; bi < nb; bi += gridDim.x)
+        my_global += agg_one(a, bi, tk0, tk1, tcnt, rlen_s, bstart, spos, wsum);
     // one atomic per workgroup (a per-wave atomic on one DevState line serialises)
-    __shared__ u64 wsum[AGG_NT / 64][4];
     for (int d = 32; d >= 1; d >>= 1) my_global += __shfl_xor(my_global, d, 64);
     u64 ms = 0;
-    if (blockIdx.x == 0)                       // k_map's stats: tokens, lds hits, global ops, long
+    if (blockIdx.x == 0 && a.mode != AGG_EMIT)  // k_map's stats: tokens, lds hits, global ops, long
         for (u32 w = tid >> 2; w < a.nsrc; w += AGG_NT / 4) ms += a.map_stats[(u64)w * 4 + (tid & 3)];
     for (int d = 32; d >= 4; d >>= 1) ms += __shfl_xor(ms, d, 64);
     if ((tid & 63) < 4) wsum[tid >> 6][tid & 3] = ms + ((tid & 63) == 2 ? my_global : 0);
@@ -147,6 +283,102 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
         u64* dst[4] = {&a.st->tokens, &a.st->lds_hits, &a.st->global_ops, &a.st->long_tokens};
         if (t) atomicAdd(dst[tid], t);
     }
+}
+
+// k_rp: pass-1 workgroup b's spill -> its AGG_Q sub-bucket regions (b, q) of pool2, q = bits 6..12
+// of the key's LDS hash (bits 0-5 are the bucket; the LDS slot choice uses the high bits).
+// Rounds of AGG_BATCH units: every lane appends its entries, whole, to its sub-bucket's LDS buffer
+// (or, when that buffer is full, straight to the region); then the buffers are written out
+// together.  The regions belong to this workgroup alone, so their cursors live in LDS too.  A full
+// region falls back to global-table inserts (exact).
+constexpr u32 RP_QB = 96;              // LDS units per sub-bucket buffer (96 KiB in all)
+__global__ __launch_bounds__(AGG_NT) void k_rp(const u64* spill, u64 spill_cap, const u32* spill_len, u64* pool2,
+                                               u64 cap2, u32* region_len2, GEntry* gtab, u64 gmask, DevState* st) {
+    __shared__ u64 sbuf[AGG_Q][RP_QB];
+    __shared__ u32 scnt[AGG_Q], sfill[AGG_Q], gpos[AGG_Q], gbase[AGG_Q];
+    __shared__ u32 sdirect[AGG_Q];            // 1: this round's buffer goes out entry by entry
+    const u32 b = blockIdx.x, tid = threadIdx.x;
+    const u32 n = spill_len[b];
+    if (n == 0) {                              // nothing spilled (low-cardinality text)
+        for (u32 q = tid; q < AGG_Q; q += AGG_NT) region_len2[(u64)b * AGG_Q + q] = 0;
+        return;
+    }
+    for (u32 q = tid; q < AGG_Q; q += AGG_NT) { scnt[q] = 0; sfill[q] = 0; gpos[q] = 0; }
+    __syncthreads();
+    const u64* src = spill + (u64)b * spill_cap;
+    u64* const dst = pool2 + (u64)b * AGG_Q * cap2;
+    u64 my_global = 0;
+    auto encode = [](u64 k0, u64 k1, u64 c, u64 (&e)[3]) {
+        const u64 f = c > 1 ? U_CNT : 0;
+        if (key_short(k0)) { e[0] = k0 | f; e[1] = c; }
+        else { e[0] = k0; e[1] = k1 | f; e[2] = c; }
+    };
+    // one whole entry into region q at a reserved place, or (past the region's end) into the
+    // global table, zero-filling the reserved units that lie inside the region (fillers)
+    auto to_region = [&](u32 q, u64 pos, const u64 (&e)[3], u32 nu, u64 k0, u64 k1, u64 c) {
+        u64* r = dst + (u64)q * cap2;
+        if (pos + nu <= cap2) { for (u32 t = 0; t < nu; t++) r[pos + t] = e[t]; return; }
+        for (u64 t = pos; t < cap2; t++) r[t] = 0;
+        my_global++;
+        ginsert(gtab, gmask, k0, k1, gslot(key_hash(k0, k1)), c, st);
+    };
+    for (u32 base = 0; base < n; base += AGG_BATCH) {
+        const u32 i0 = base + 4 * tid;
+        u64 u[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) u[j] = i0 + j < n ? src[i0 + j] : 0;
+        u64 k0[4], k1[4], c[4];
+        bool v[4];
+        u32 nu[4];
+        agg_decode(u, k0, k1, c, v, nu);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (!v[j]) continue;
+            const u32 q = (lds_hash(k0[j], k1[j]) >> 6) & (AGG_Q - 1);
+            u64 e[3];
+            encode(k0[j], k1[j], c[j], e);
+            const u32 pos = atomicAdd(&scnt[q], nu[j]);
+            if (pos + nu[j] <= RP_QB) {        // the entries that fit are a prefix of the buffer
+                for (u32 t = 0; t < nu[j]; t++) sbuf[q][pos + t] = e[t];
+                atomicMax(&sfill[q], pos + nu[j]);
+            } else {
+                to_region(q, atomicAdd(&gpos[q], nu[j]), e, nu[j], k0[j], k1[j], c[j]);
+            }
+        }
+        __syncthreads();
+        for (u32 q = tid; q < AGG_Q; q += AGG_NT) {         // reserve each buffer's place
+            gbase[q] = gpos[q];
+            gpos[q] += sfill[q];
+            sdirect[q] = (u64)gbase[q] + sfill[q] > cap2;
+        }
+        __syncthreads();
+        for (u32 t = tid; t < AGG_Q * RP_QB; t += AGG_NT) {  // write the buffers out
+            const u32 q = t / RP_QB, j = t % RP_QB;
+            if (j < sfill[q] && !sdirect[q]) dst[(u64)q * cap2 + gbase[q] + j] = sbuf[q][j];
+        }
+        for (u32 q = tid; q < AGG_Q; q += AGG_NT) {         // a buffer running past its region
+            if (!sdirect[q]) continue;                        // (rare): entry by entry
+            u64 pos = gbase[q];
+            for (u32 j = 0; j < sfill[q];) {
+                u64 y[6] = {sbuf[q][j], j + 1 < sfill[q] ? sbuf[q][j + 1] : 0, j + 2 < sfill[q] ? sbuf[q][j + 2] : 0, 0, 0, 0};
+                u64 kk0[4], kk1[4], cc[4];
+                bool vv[4];
+                u32 nn[4];
+                agg_decode(y, kk0, kk1, cc, vv, nn);
+                u64 e[3];
+                encode(kk0[0], kk1[0], cc[0], e);
+                to_region(q, pos, e, nn[0], kk0[0], kk1[0], cc[0]);
+                pos += nn[0];
+                j += nn[0];
+            }
+        }
+        __syncthreads();
+        for (u32 q = tid; q < AGG_Q; q += AGG_NT) { scnt[q] = 0; sfill[q] = 0; }
+        __syncthreads();
+    }
+    for (u32 q = tid; q < AGG_Q; q += AGG_NT) region_len2[(u64)b * AGG_Q + q] = gpos[q] < cap2 ? gpos[q] : (u32)cap2;
+    for (int d = 32; d >= 1; d >>= 1) my_global += __shfl_xor(my_global, d, 64);
+    if ((tid & 63) == 0 && my_global) atomicAdd(&st->global_ops, my_global);
 }
 
 }  // namespace wcg

@@ -52,6 +52,11 @@ struct wcg_ctx {
     u32* bid = nullptr; u64 bid_cap = 0;
     Rec* irec = nullptr; u64 irec_cap = 0;
     LEnt* lent = nullptr; u64 lent_cap = 0;   // long-key partitions: LQ x lpart_cap entries
+    u64* spill = nullptr; u64 spill_cap = 0;  // k_agg pass-1 spill regions
+    u32* spill_len = nullptr; u64 spill_len_cap = 0;
+    u64* pool2 = nullptr; u64 pool2_cap = 0;  // k_rp sub-bucket regions
+    u32* rlen2 = nullptr; u64 rlen2_cap = 0;
+    Rec* remit = nullptr; u64 remit_cap = 0;  // record log of k_agg's pass 2
     u32* lpcur = nullptr; u64 lpcur_cap = 0;    // 2n records: by bucket, and the oversized-bucket scratch
     u32* hist = nullptr; u64 hist_cap = 0;    // [B][G] bucket counts / partition counts
     u64* spart = nullptr; u64 spart_cap = 0;  // multi-block scan partials
@@ -212,6 +217,9 @@ int compact(wcg_ctx* c) {
     for (int pass = 0; pass < 2; pass++) {
         HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));   // nrec, nlong
         if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
+        if (c->remit)                  // the record log of k_agg's pass 2 first (nrec = nemit)
+            k_copy_emit<<<(unsigned)(c->ncu * 4), 256, 0, c->stream>>>(
+                c->remit, c->recA, std::min<u64>(c->rec_cap, c->max_keys + 65536), c->st);
         const u64 total = c->gslots + c->lslots;
         k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
             c->gtab, c->gslots, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st);
@@ -347,6 +355,17 @@ int sort_records(wcg_ctx* c) {
     HIPCHK(c, hipGetLastError());
     if (c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA));
     c->compacted = false;          // recA was scratch for the ties
+    if (c->h_st->nemit) {          // the record log: keys may repeat (k_dd_*, wcg_sort.h)
+        RC(ensure(c, &c->bid, &c->bid_cap, n));
+        k_dd_flag<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recB, n, c->bid);
+        RC(scan_u32(c, c->bid, n));
+        k_dd_write<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recB, n, c->bid, c->recA, c->d_scalar);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->nrec = *c->h_scalar;
+        c->sorted = c->recA;
+    }
     return WCG_OK;
 }
 
@@ -575,7 +594,7 @@ int wcg_close(wcg_ctx* c) {
     }
     void* bufs[] = {c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens, c->d_scalar, c->d_out,
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
-                    c->llog, c->llog_len, c->smp, c->bid, c->irec, c->lent, c->lpcur, c->hist, c->spart, c->ikey, c->iidx, c->groups,
+                    c->llog, c->llog_len, c->smp, c->bid, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->hist, c->spart, c->ikey, c->iidx, c->groups,
                     c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
@@ -726,15 +745,47 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         k_long_agg<<<LQ, LONG_NT, 0, c->stream>>>(a, lp);
         HIPCHK(c, hipGetLastError());
     }
+    // k_agg pass 1 (spills what its LDS tables cannot hold) -> k_rp -> pass 2 (wcg_agg.h)
     AggArgs g;
     g.pool = c->pool; g.region_len = c->region_len; g.region_cap = a.region_cap;
     g.P = P; g.nsrc = (u32)grid;
     g.slices = std::max<u32>(1, std::min<u32>((u32)grid, (u32)(c->ncu + P - 1) / P));
     g.slices = std::max<u32>(g.slices, (u32)((grid + AGG_MAX_SRC - 1) / AGG_MAX_SRC));
+    g.rstride = P; g.rmod = P; g.P1 = P; g.mode = AGG_SPILL;
     g.gtab = c->gtab; g.gmask = c->gslots - 1; g.st = c->st;
     g.map_stats = c->wg_stats;
-    k_agg<<<P * g.slices, AGG_NT, 0, c->stream>>>(g);
+    const u32 nb1 = P * g.slices;
+    // Two passes only for high-cardinality jobs (the table is sized for more than 4M keys, or
+    // WCG_AGG_TWO_PASS=1): on low-cardinality text nothing spills, and the extra launches and the
+    // record-log merge would only cost time.  One pass sends an entry its LDS table cannot take
+    // to the global table.
+    static const char* tp_env = getenv("WCG_AGG_TWO_PASS");
+    const bool two_pass = tp_env ? atoi(tp_env) != 0 : c->max_keys > (4ull << 20);
+    // a workgroup spills at most what it reads: its slice's regions
+    g.spill_cap = two_pass ? (u64)cdiv(grid, g.slices) * a.region_cap : 0;
+    RC(ensure(c, &c->spill, &c->spill_cap, std::max<u64>(nb1 * g.spill_cap, 1)));
+    RC(ensure(c, &c->spill_len, &c->spill_len_cap, (u64)nb1));
+    g.spill = c->spill; g.spill_len = c->spill_len;
+    const u64 rec_cap_emit = c->max_keys + 65536;
+    RC(ensure(c, &c->remit, &c->remit_cap, rec_cap_emit));
+    g.emit = c->remit; g.emit_cap = rec_cap_emit;
+    k_agg<<<nb1, AGG_NT, 0, c->stream>>>(g);
     HIPCHK(c, hipGetLastError());
+    if (two_pass) {
+    // sub-bucket regions: 1.5x an even share of a spill region, a full one falls back to exact
+    // global inserts
+    const u64 cap2 = ((g.spill_cap * 3 / 2) / AGG_Q + 1024) & ~1ull;
+    RC(ensure(c, &c->pool2, &c->pool2_cap, (u64)nb1 * AGG_Q * cap2 + AGG_SLACK_UNITS));
+    RC(ensure(c, &c->rlen2, &c->rlen2_cap, (u64)nb1 * AGG_Q));
+    k_rp<<<nb1, AGG_NT, 0, c->stream>>>(c->spill, g.spill_cap, c->spill_len, c->pool2, cap2, c->rlen2, c->gtab,
+                                        c->gslots - 1, c->st);
+    AggArgs g2 = g;
+    g2.pool = c->pool2; g2.region_len = c->rlen2; g2.region_cap = cap2;
+    g2.P = P * AGG_Q; g2.nsrc = g.slices; g2.slices = 1;
+    g2.rstride = AGG_Q; g2.rmod = AGG_Q; g2.P1 = P; g2.mode = AGG_EMIT;
+    k_agg<<<std::min<u32>(P * AGG_Q, (u32)c->ncu * 2), AGG_NT, 0, c->stream>>>(g2);
+    HIPCHK(c, hipGetLastError());
+    }
     if (c->timing) {
         e2 = take_event(c);
         HIPCHK(c, hipEventRecord(e2, c->stream));
@@ -1077,7 +1128,7 @@ int wcg_timings(wcg_ctx* c, double* ms, int n, uint64_t* map_launches) {
     return WCG_OK;
 }
 
-int wcg_stats(wcg_ctx* c, uint64_t* s8) {
+int wcg_stats(wcg_ctx* c, uint64_t* s8) {   // 9 values (include/wcg.h)
     if (!c || !s8) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
@@ -1085,6 +1136,7 @@ int wcg_stats(wcg_ctx* c, uint64_t* s8) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     s8[0] = c->h_st->tokens; s8[1] = c->nrec; s8[2] = c->h_st->lds_hits; s8[3] = c->h_st->global_ops;
     s8[4] = c->h_st->long_tokens; s8[5] = c->h_st->arena_top; s8[6] = c->h_st->overflow; s8[7] = c->h_st->spin_fail;
+    s8[8] = c->h_st->nemit;
     return WCG_OK;
 }
 

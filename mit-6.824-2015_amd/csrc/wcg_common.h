@@ -79,6 +79,7 @@ struct DevState {
     u64 arena_top;       // bytes used in the long-key arena heap (keys > 32 B; shorter keys use slot cells)
     u64 nrec;            // records produced by compaction
     u64 nlong;           // ... of which long keys (> 15 bytes)
+    u64 nemit;           // records emitted by k_agg's pass 2 (the record log, across map calls)
     u32 overflow;        // table / arena full -> WCG_EFULL
     u32 spin_fail;       // bounded spin gave up -> WCG_EFULL (never expected)
     u32 bad_input;       // malformed record units (wcg_import) or lines (wcg_merge_runs) -> WCG_EINVAL

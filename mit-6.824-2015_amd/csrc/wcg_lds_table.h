@@ -41,9 +41,13 @@ struct LdsTable {
         }
     }
 
+    // b1 from the high bits of h; b2 from all of h, mixed: the low bits select the miss bucket
+    // (pass 1) and the sub-bucket (pass 2), so they are constant within a workgroup's keys
     __device__ __forceinline__ static void buckets(u32 h, u32& b1, u32& b2) {
         b1 = __umulhi(h, (u32)NB);
-        b2 = __umulhi(__builtin_rotateleft32(h, 16), (u32)NB);
+        u32 m = h * 0x85EBCA6Bu;
+        m ^= m >> 15;
+        b2 = __umulhi(m * 0xC2B2AE35u, (u32)NB);
         if (b2 == b1) b2 = (b1 + 1 == (u32)NB) ? 0 : b1 + 1;
     }
 

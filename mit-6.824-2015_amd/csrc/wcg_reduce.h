@@ -88,6 +88,14 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
         if (have & (1u << j)) { if (pos < cap) out[pos] = r[j]; pos++; }   // more: host grows, reruns
 }
 
+// the record log of k_agg's pass 2 -> the front of the compaction output (nrec = its length;
+// k_agg sent records past the log's capacity to the global table)
+__global__ void k_copy_emit(const Rec* src, Rec* dst, u64 cap, DevState* st) {
+    const u64 n = st->nemit, m = n < cap ? n : cap;
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < m; i += (u64)gridDim.x * blockDim.x) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->nrec = m;
+}
+
 // ---------------------------------------------------------------- formatting
 // decimal digits of a count: compares against powers of ten (a u64 division is a long software
 // routine on the GPU)

@@ -538,6 +538,32 @@ __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
     for (u32 j = threadIdx.x; j < m; j += SB_NT) a.out[s + j] = X[kp[j]];
 }
 
+// ---------------------------------------------------------------- duplicate keys
+// The record log of k_agg's pass 2 and the compacted tables may hold one key more than once
+// (pass-1 flushes, other map calls): after the sort such records are adjacent.  Inline records
+// only (long keys live in the long-key table alone): equal (hi, lo, ref = length).
+__device__ __forceinline__ bool dd_head(const Rec* r, u64 i) {
+    if (i == 0) return true;
+    const Rec& x = r[i];
+    const Rec& y = r[i - 1];
+    return (x.ref & LONG_FLAG) || (y.ref & LONG_FLAG) || x.hi != y.hi || x.lo != y.lo || x.ref != y.ref;
+}
+__global__ void k_dd_flag(const Rec* r, u64 n, u32* flag) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
+        flag[i] = dd_head(r, i) ? 1u : 0u;
+}
+// after an exclusive scan of the flags: each head sums its run into out[pos]; the last thread
+// writes the number of heads
+__global__ void k_dd_write(const Rec* r, u64 n, const u32* pos, Rec* out, u64* nout) {
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        if (i == n - 1) *nout = (u64)pos[i] + (dd_head(r, i) ? 1 : 0);
+        if (!dd_head(r, i)) continue;
+        Rec x = r[i];
+        for (u64 j = i + 1; j < n && !dd_head(r, j); j++) x.cnt += r[j].cnt;
+        out[pos[i]] = x;
+    }
+}
+
 // ---------------------------------------------------------------- tie groups
 __device__ __forceinline__ u64 ik_hi(uint4 k) { return (u64)k.w << 32 | k.z; }
 __device__ __forceinline__ u64 ik_lo(uint4 k) { return (u64)k.y << 32 | k.x; }

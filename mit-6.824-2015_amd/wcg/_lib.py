@@ -295,10 +295,10 @@ class Engine:
         return dict(zip(self.PHASES, list(ms))), nl.value
 
     def stats(self) -> dict:
-        s = (ctypes.c_uint64 * 8)()
+        s = (ctypes.c_uint64 * 9)()
         self._chk(self._lib.wcg_stats(self._ctx, s))
         keys = ["tokens", "keys", "lds_hits", "global_ops", "long_tokens", "arena_bytes", "overflow",
-                "spin_fail"]
+                "spin_fail", "emitted"]
         return dict(zip(keys, list(s)))
 
 

@@ -247,3 +247,24 @@ def test_long_token_lengths(built, shape):
         e.reduce()
         ob.assert_same(e.result(), ob.merged(data))
         assert e.stats()["overflow"] == 0
+
+
+def test_high_cardinality_spill_and_record_log(built):
+    """~3M distinct inline keys over two map calls that share a third of them: k_agg's pass-1
+    tables overflow, entries spill to k_rp's sub-buckets, pass 2 emits records, and the keys
+    counted in both calls (and in the pass-1 flushes) are merged after the sort."""
+    import wcg
+    rng = random.Random(9)
+    alpha = b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJ"
+    keys = list({bytes(rng.choice(alpha) for _ in range(rng.randrange(3, 16))) for _ in range(3_100_000)})
+    third = len(keys) // 3
+    d1 = b" ".join(keys[: 2 * third] + keys[:50_000]) + b"\n"
+    d2 = b" ".join(keys[third:] + keys[:50_000]) + b"\n"
+    with wcg.Engine(0, 0, 8_000_000) as e:        # > 4M keys: the two-pass aggregation
+        e.reset()
+        e.map_host(d1)
+        e.map_host(d2)
+        e.reduce()
+        ob.assert_same(e.result(), ob.merged(d1 + d2))
+        st = e.stats()
+        assert st["keys"] == len(keys) and st["emitted"] > 0
