@@ -161,7 +161,7 @@ WCG_API int wcg_merge_runs(wcg_ctx *ctx, const void *dev_text, const uint64_t *r
 /* Per-phase device time of the last pipeline run, in milliseconds, measured with HIP events
  * on the context's stream: ms[0] map kernel (tokenize + LDS aggregation, summed over the
  * wcg_map* calls since wcg_reset), ms[1] long-token counting + miss-log aggregation kernels
- * (k_long, k_agg), ms[2] compaction,
+ * (k_long_hash, k_long_agg, k_agg pass 1, k_rp, k_agg pass 2), ms[2] compaction,
  * ms[3] sort, ms[4] format.  n = number of doubles the caller provides (<= 5). */
 WCG_API int wcg_timings(wcg_ctx *ctx, double *ms, int n, uint64_t *map_launches);
 /* Enable/disable the event timing above (off by default: it adds event records). */
