@@ -13,7 +13,7 @@
 // spills.  High-cardinality text (C4: 22M distinct inline keys per GiB, 347K per bucket against
 // 6,760 LDS slots) spills nearly everything, and per-occurrence global inserts of the spilled
 // entries were 5.8 of a 19 ms step.
-// k_rp: each pass-1 workgroup's spill is split by 7 more hash bits into AGG_Q sub-buckets (LDS
+// k_rp: each pass-1 workgroup's spill is split by 7 bits of another hash into AGG_Q sub-buckets (LDS
 // staging, whole entries), so a sub-bucket holds ~1/8192 of the keys.
 // Pass 2 (k_agg, mode AGG_EMIT): one workgroup per (p, q) sub-bucket aggregates it in LDS and emits
 // each distinct key as a record straight into the record log (no global-table insert); the
@@ -74,6 +74,11 @@ __device__ __forceinline__ Rec inline_rec(u64 k0, u64 k1, u64 cnt) {
     r.cnt = cnt;
     return r;
 }
+
+// bucket choices of the aggregation tables: the high half of the 64-bit key hash.  k_map's
+// 32-bit LDS hash (one multiply from the key bytes, chosen for k_map's hot path) gave C4's UTF-8
+// keys so many equal values that both choices of some keys were full in pass 2.
+__device__ __forceinline__ u32 agg_hash(u64 k0, u64 k1) { return (u32)(key_hash(k0, k1) >> 32); }
 
 // decode the entries headed by 4 of a lane's units (u[0..6): its 4 units and the 2 after them;
 // units past the region are 0 = filler)
@@ -191,8 +196,8 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
             typename decltype(tab)::Probe pa, pb;
-            if (v[j]) tab.start(lds_hash(k0[j], k1[j]), pa);
-            if (v[j + 1]) tab.start(lds_hash(k0[j + 1], k1[j + 1]), pb);
+            if (v[j]) tab.start(agg_hash(k0[j], k1[j]), pa);
+            if (v[j + 1]) tab.start(agg_hash(k0[j + 1], k1[j + 1]), pb);
             if (v[j] && !tab.finish(k0[j], k1[j], pa, c[j])) overflow(k0[j], k1[j], c[j], nu[j]);
             if (v[j + 1] && !tab.finish(k0[j + 1], k1[j + 1], pb, c[j + 1])) overflow(k0[j + 1], k1[j + 1], c[j + 1], nu[j + 1]);
         }
@@ -216,15 +221,20 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
         load(kb, bb, b0, b1, b2);
     }
     __syncthreads();
-    if (!emit && tid == 0) a.spill_len[bi] = spos < a.spill_cap ? spos : (u32)a.spill_cap;
     if (!emit) {
+        // one-pass mode: the table goes to the global table (one insert per slice and key);
+        // two-pass mode: it is spilled too, so every inline key of the bucket reaches exactly one
+        // pass-2 sub-bucket and is emitted once per map call (no duplicate with the global table)
         for (int i = tid; i < AGG_NB * AGG_W; i += AGG_NT) {
             const u64 c = (&tcnt[0][0])[i];
             if (!c) continue;
             const u64 k0 = (&tk0[0][0])[i], k1 = (&tk1[0][0])[i];
+            if (a.spill_cap) { overflow(k0, k1, c, (u32)entry_units(k0, (u32)(c > 1 ? 2 : 1))); continue; }
             my_global++;
             ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
         }
+        __syncthreads();
+        if (tid == 0) a.spill_len[bi] = spos < a.spill_cap ? spos : (u32)a.spill_cap;
     } else {
         // pass 2: this sub-bucket's keys, one record each, placed by one atomic per workgroup;
         // positions past the log's end go to the global table instead (the log stays dense:
@@ -285,8 +295,9 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     }
 }
 
-// k_rp: pass-1 workgroup b's spill -> its AGG_Q sub-bucket regions (b, q) of pool2, q = bits 6..12
-// of the key's LDS hash (bits 0-5 are the bucket; the LDS slot choice uses the high bits).
+// k_rp: pass-1 workgroup b's spill -> its AGG_Q sub-bucket regions (b, q) of pool2, q = 7 bits of
+// the key's 64-bit hash (the 32-bit LDS hash's low bits, a single multiply away from the key
+// bytes, left C4's UTF-8 keys unevenly spread: sub-buckets overflowed their LDS tables).
 // Rounds of AGG_BATCH units: every lane appends its entries, whole, to its sub-bucket's LDS buffer
 // (or, when that buffer is full, straight to the region); then the buffers are written out
 // together.  The regions belong to this workgroup alone, so their cursors live in LDS too.  A full
@@ -334,7 +345,7 @@ __global__ __launch_bounds__(AGG_NT) void k_rp(const u64* spill, u64 spill_cap, 
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             if (!v[j]) continue;
-            const u32 q = (lds_hash(k0[j], k1[j]) >> 6) & (AGG_Q - 1);
+            const u32 q = (u32)(key_hash(k0[j], k1[j]) >> 40) & (AGG_Q - 1);
             u64 e[3];
             encode(k0[j], k1[j], c[j], e);
             const u32 pos = atomicAdd(&scnt[q], nu[j]);

@@ -46,6 +46,7 @@ struct wcg_ctx {
     u64* h_scalar = nullptr;                  // pinned scratch (64 u64)
     uint8_t* d_out = nullptr; u64 out_cap = 0; u64 out_len = 0;
     u64 nrec = 0;
+    u64 nkeys = 0;                            // distinct keys among the nrec sorted records
     bool compacted = false, reduced = false;
     // sort (wcg_sort.h)
     Rec* smp = nullptr; u64 smp_cap = 0;      // 2 x sample records (merge ping-pong)
@@ -57,6 +58,8 @@ struct wcg_ctx {
     u64* pool2 = nullptr; u64 pool2_cap = 0;  // k_rp sub-bucket regions
     u32* rlen2 = nullptr; u64 rlen2_cap = 0;
     Rec* remit = nullptr; u64 remit_cap = 0;  // record log of k_agg's pass 2
+    bool two_pass_used = false;               // a map call since wcg_reset ran the two passes
+    bool imported = false;                    // wcg_import since wcg_reset
     u32* lpcur = nullptr; u64 lpcur_cap = 0;    // 2n records: by bucket, and the oversized-bucket scratch
     u32* hist = nullptr; u64 hist_cap = 0;    // [B][G] bucket counts / partition counts
     u64* spart = nullptr; u64 spart_cap = 0;  // multi-block scan partials
@@ -214,15 +217,24 @@ int ensure_recs(wcg_ctx* c, u64 n) {
 // runs again) when the tables hold more keys than that
 int compact(wcg_ctx* c) {
     if (c->compacted) return WCG_OK;
+    // Two-pass jobs emit their inline keys as records; when nothing else reached the global
+    // table (no fallback insert, no import), its slots are all empty and the scan is skipped.
+    bool scan_gtab = true;
+    if (c->two_pass_used && !c->imported) {
+        HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        scan_gtab = c->h_st->global_ops != 0;
+    }
     for (int pass = 0; pass < 2; pass++) {
         HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));   // nrec, nlong
         if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
         if (c->remit)                  // the record log of k_agg's pass 2 first (nrec = nemit)
             k_copy_emit<<<(unsigned)(c->ncu * 4), 256, 0, c->stream>>>(
                 c->remit, c->recA, std::min<u64>(c->rec_cap, c->max_keys + 65536), c->st);
-        const u64 total = c->gslots + c->lslots;
+        const u64 gs = scan_gtab ? c->gslots : 0;
+        const u64 total = gs + c->lslots;
         k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
-            c->gtab, c->gslots, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st);
+            c->gtab, gs, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st);
         HIPCHK(c, hipGetLastError());
         if (c->timing) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
         RC(check_status(c));
@@ -306,6 +318,7 @@ int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp) {
 // sample sort of recA[0:nrec) into recB (wcg_sort.h), then the tie groups
 int sort_records(wcg_ctx* c) {
     const u64 n = c->nrec;
+    c->nkeys = n;
     c->sorted = c->recB;
     if (n == 0) return WCG_OK;
     if (n == 1) {
@@ -355,16 +368,19 @@ int sort_records(wcg_ctx* c) {
     HIPCHK(c, hipGetLastError());
     if (c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA));
     c->compacted = false;          // recA was scratch for the ties
-    if (c->h_st->nemit) {          // the record log: keys may repeat (k_dd_*, wcg_sort.h)
-        RC(ensure(c, &c->bid, &c->bid_cap, n));
-        k_dd_flag<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recB, n, c->bid);
-        RC(scan_u32(c, c->bid, n));
-        k_dd_write<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recB, n, c->bid, c->recA, c->d_scalar);
+    if (getenv("WCG_DEBUG"))
+        fprintf(stderr, "wcg: nemit %llu global_ops %llu\n", (unsigned long long)c->h_st->nemit,
+                (unsigned long long)c->h_st->global_ops);
+    // the record log: a key may repeat (the global table, other map calls, racing inserts of one
+    // key in pass 2): duplicates merged in place (k_dd_merge, wcg_sort.h)
+    c->nkeys = n;
+    if (c->h_st->nemit) {
+        HIPCHK(c, hipMemsetAsync(c->d_scalar, 0, sizeof(u64), c->stream));
+        k_dd_merge<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recB, n, c->d_scalar);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        c->nrec = *c->h_scalar;
-        c->sorted = c->recA;
+        c->nkeys = *c->h_scalar;
     }
     return WCG_OK;
 }
@@ -636,6 +652,8 @@ int wcg_reset(wcg_ctx* c) {
     c->ev_used = 0;
     c->phase_rec = false;
     c->map_launches = 0;
+    c->two_pass_used = false;
+    c->imported = false;
     return WCG_OK;
 }
 
@@ -772,6 +790,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     k_agg<<<nb1, AGG_NT, 0, c->stream>>>(g);
     HIPCHK(c, hipGetLastError());
     if (two_pass) {
+    c->two_pass_used = true;
     // sub-bucket regions: 1.5x an even share of a spill region, a full one falls back to exact
     // global inserts
     const u64 cap2 = ((g.spill_cap * 3 / 2) / AGG_Q + 1024) & ~1ull;
@@ -851,7 +870,7 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
     }
     c->reduced = true;
     c->part_R = 0;
-    if (nkeys) *nkeys = c->nrec;
+    if (nkeys) *nkeys = c->nkeys;
     if (nbytes) *nbytes = c->out_len;
     return WCG_OK;
 }
@@ -998,6 +1017,7 @@ int wcg_import(wcg_ctx* c, const void* dev_records, uint64_t nrecords) {
                                                                           c->gslots - 1, c->ltab, c->lslots - 1,
                                                                           c->arena, c->arena_cap, c->st);
     HIPCHK(c, hipGetLastError());
+    c->imported = true;
     c->compacted = c->reduced = false;
     c->exp_ready = false;
     c->part_R = 0;
@@ -1016,7 +1036,7 @@ int wcg_merge_runs(wcg_ctx* c, const void* dev_text, const uint64_t* run_bytes, 
     c->part_R = 0;
     c->reduced = false;
     if (total == 0) {
-        c->nrec = 0; c->out_len = 0; c->reduced = true;
+        c->nrec = 0; c->nkeys = 0; c->out_len = 0; c->reduced = true;
         if (nkeys) *nkeys = 0;
         if (nbytes) *nbytes = 0;
         return WCG_OK;
@@ -1062,6 +1082,7 @@ int wcg_merge_runs(wcg_ctx* c, const void* dev_text, const uint64_t* run_bytes, 
     }
     c->sorted = src;
     c->nrec = L;
+    c->nkeys = L;
     RC(fix_ties(c, src, L, text, dst));
     RC(dbg(c, "merge_runs: ties"));
     RC(format(c, src, L, text, FMT_COPY, 1, 0, total, &c->d_out, &c->out_cap, &c->out_len));
@@ -1134,7 +1155,7 @@ int wcg_stats(wcg_ctx* c, uint64_t* s8) {   // 9 values (include/wcg.h)
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    s8[0] = c->h_st->tokens; s8[1] = c->nrec; s8[2] = c->h_st->lds_hits; s8[3] = c->h_st->global_ops;
+    s8[0] = c->h_st->tokens; s8[1] = c->reduced ? c->nkeys : c->nrec; s8[2] = c->h_st->lds_hits; s8[3] = c->h_st->global_ops;
     s8[4] = c->h_st->long_tokens; s8[5] = c->h_st->arena_top; s8[6] = c->h_st->overflow; s8[7] = c->h_st->spin_fail;
     s8[8] = c->h_st->nemit;
     return WCG_OK;

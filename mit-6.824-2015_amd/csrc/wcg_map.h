@@ -323,7 +323,7 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
         u64 len = r >> 40, h = 0;
         if (i < nrec && len == 0) {
             len = long_walk(a, p, &h);
-            if (len <= 15) { count_inline_run(a, p, len); len = 0; }
+            if (len <= 15) { count_inline_run(a, p, len); atomicAdd(&a.st->global_ops, 1ull); len = 0; }
             else if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); len = 0; }
         } else if (len != 0) {
             h = 0xCBF29CE484222325ull;

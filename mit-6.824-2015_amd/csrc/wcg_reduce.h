@@ -140,7 +140,9 @@ __device__ u32 rec_ihash(const Rec& r, const uint8_t* arena) {
 constexpr int FMT_MERGED = 0, FMT_JSON = 1, FMT_JSON_ALL = 2, FMT_COPY = 3;
 constexpr u64 JSON_FIXED = 8 + 11 + 3;   // {"Key":" + ","Value":" + "}\n
 
+// a record with count 0 is a merged duplicate (k_dd_merge, wcg_sort.h): no line
 __device__ __forceinline__ u64 line_len(const Rec& x, int fmt, u32 nreduce, u32 part, const uint8_t* arena) {
+    if (x.cnt == 0 && fmt != FMT_COPY) return 0;
     if (fmt == FMT_MERGED) return rec_len(x) + 3 + ndigits(x.cnt);
     if (fmt == FMT_COPY) return x.cnt;
     if (fmt == FMT_JSON_ALL) return rec_len(x) + JSON_FIXED + ndigits(x.cnt);
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(PT_NT) void k_part_hist(const Rec* r, u64 n, u32 R,
         const u32 p = rec_ihash(x, arena) % R;
         pid[i] = p;
         atomicAdd(&c[p], 1u);
-        atomicAdd((unsigned long long*)&bsum[p], (unsigned long long)(rec_len(x) + JSON_FIXED + ndigits(x.cnt)));
+        if (x.cnt) atomicAdd((unsigned long long*)&bsum[p], (unsigned long long)(rec_len(x) + JSON_FIXED + ndigits(x.cnt)));
     }
     __syncthreads();
     for (u32 p = threadIdx.x; p < R; p += PT_NT) {

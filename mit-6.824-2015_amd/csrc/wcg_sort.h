@@ -540,28 +540,30 @@ __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
 
 // ---------------------------------------------------------------- duplicate keys
 // The record log of k_agg's pass 2 and the compacted tables may hold one key more than once
-// (pass-1 flushes, other map calls): after the sort such records are adjacent.  Inline records
-// only (long keys live in the long-key table alone): equal (hi, lo, ref = length).
+// (the global table, other map calls, two slots claimed for one key by racing lanes): after the
+// sort such records are adjacent.  Inline records only (long keys live in the long-key table
+// alone): equal (hi, lo, ref = length).  Merged in place: the first record of a run takes the
+// run's total and the others count 0, which formats to no line (wcg_reduce.h: line_len); the
+// number of distinct keys goes to *nkeys.
 __device__ __forceinline__ bool dd_head(const Rec* r, u64 i) {
     if (i == 0) return true;
     const Rec& x = r[i];
     const Rec& y = r[i - 1];
     return (x.ref & LONG_FLAG) || (y.ref & LONG_FLAG) || x.hi != y.hi || x.lo != y.lo || x.ref != y.ref;
 }
-__global__ void k_dd_flag(const Rec* r, u64 n, u32* flag) {
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x)
-        flag[i] = dd_head(r, i) ? 1u : 0u;
-}
-// after an exclusive scan of the flags: each head sums its run into out[pos]; the last thread
-// writes the number of heads
-__global__ void k_dd_write(const Rec* r, u64 n, const u32* pos, Rec* out, u64* nout) {
+__global__ void k_dd_merge(Rec* r, u64 n, u64* nkeys) {
+    u64 heads = 0;
     for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        if (i == n - 1) *nout = (u64)pos[i] + (dd_head(r, i) ? 1 : 0);
         if (!dd_head(r, i)) continue;
-        Rec x = r[i];
-        for (u64 j = i + 1; j < n && !dd_head(r, j); j++) x.cnt += r[j].cnt;
-        out[pos[i]] = x;
+        heads++;
+        u64 j = i + 1;
+        if (j >= n || dd_head(r, j)) continue;      // no duplicate (nearly always)
+        u64 sum = r[i].cnt;
+        for (; j < n && !dd_head(r, j); j++) { sum += r[j].cnt; r[j].cnt = 0; }
+        r[i].cnt = sum;
     }
+    for (int d = 32; d >= 1; d >>= 1) heads += __shfl_xor(heads, d, 64);
+    if ((threadIdx.x & 63) == 0 && heads) atomicAdd((unsigned long long*)nkeys, (unsigned long long)heads);
 }
 
 // ---------------------------------------------------------------- tie groups

@@ -249,10 +249,12 @@ def test_long_token_lengths(built, shape):
         assert e.stats()["overflow"] == 0
 
 
-def test_high_cardinality_spill_and_record_log(built):
-    """~3M distinct inline keys over two map calls that share a third of them: k_agg's pass-1
-    tables overflow, entries spill to k_rp's sub-buckets, pass 2 emits records, and the keys
-    counted in both calls (and in the pass-1 flushes) are merged after the sort."""
+@pytest.mark.parametrize("calls", [1, 2])
+def test_high_cardinality_spill_and_record_log(built, calls):
+    """~3M distinct inline keys (one map call, or two that share a third of them): k_agg's pass-1
+    tables overflow, entries and table flushes spill to k_rp's sub-buckets, pass 2 emits each key
+    as a record; one call emits every key once (no merge, no global-table scan), two calls emit
+    shared keys twice and the records are merged after the sort."""
     import wcg
     rng = random.Random(9)
     alpha = b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJ"
@@ -263,8 +265,10 @@ def test_high_cardinality_spill_and_record_log(built):
     with wcg.Engine(0, 0, 8_000_000) as e:        # > 4M keys: the two-pass aggregation
         e.reset()
         e.map_host(d1)
-        e.map_host(d2)
+        if calls == 2:
+            e.map_host(d2)
         e.reduce()
-        ob.assert_same(e.result(), ob.merged(d1 + d2))
+        data = d1 + d2 if calls == 2 else d1
+        ob.assert_same(e.result(), ob.merged(data))
         st = e.stats()
-        assert st["keys"] == len(keys) and st["emitted"] > 0
+        assert st["keys"] == (len(keys) if calls == 2 else 2 * third) and st["emitted"] > 0
