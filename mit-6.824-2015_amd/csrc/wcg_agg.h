@@ -75,9 +75,9 @@ __device__ __forceinline__ Rec inline_rec(u64 k0, u64 k1, u64 cnt) {
     return r;
 }
 
-// bucket choices of the aggregation tables: the high half of the 64-bit key hash.  k_map's
-// 32-bit LDS hash (one multiply from the key bytes, chosen for k_map's hot path) gave C4's UTF-8
-// keys so many equal values that both choices of some keys were full in pass 2.
+// bucket choices of pass 2's tables: the high half of the 64-bit key hash (a sub-bucket's keys
+// share 13 bits of the 32-bit LDS hash, which pass 1 uses: it is cheaper and its keys vary in all
+// bits)
 __device__ __forceinline__ u32 agg_hash(u64 k0, u64 k1) { return (u32)(key_hash(k0, k1) >> 32); }
 
 // decode the entries headed by 4 of a lane's units (u[0..6): its 4 units and the 2 after them;
@@ -166,7 +166,15 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
     constexpr u32 WSTRIDE = AGG_NT / 64;
     // (region k, batch b) of a wave's batch g, advanced incrementally: g grows by WSTRIDE per
     // step, which crosses at most a few region ends
+    // Pass 1 (64 regions per workgroup) walks a region per wave instead (k, k + 16, ...): measured
+    // 10% faster there than the round-robin deal, which pass 2 (4 regions) needs.
+    const bool per_wave = !emit;
     auto advance = [&](u32& k, u32& b, u32 step) {
+        if (per_wave) {
+            b += step / WSTRIDE;                      // one batch of the wave's own region
+            while (k < nk && b >= bstart[k + 1] - bstart[k]) { k += WSTRIDE; b = 0; }
+            return;
+        }
         b += step;
         while (k < nk) {
             const u32 nbk = bstart[k + 1] - bstart[k];
@@ -196,14 +204,15 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
             typename decltype(tab)::Probe pa, pb;
-            if (v[j]) tab.start(agg_hash(k0[j], k1[j]), pa);
-            if (v[j + 1]) tab.start(agg_hash(k0[j + 1], k1[j + 1]), pb);
+            if (v[j]) tab.start(emit ? agg_hash(k0[j], k1[j]) : lds_hash(k0[j], k1[j]), pa);
+            if (v[j + 1]) tab.start(emit ? agg_hash(k0[j + 1], k1[j + 1]) : lds_hash(k0[j + 1], k1[j + 1]), pb);
             if (v[j] && !tab.finish(k0[j], k1[j], pa, c[j])) overflow(k0[j], k1[j], c[j], nu[j]);
             if (v[j + 1] && !tab.finish(k0[j + 1], k1[j + 1], pb, c[j + 1])) overflow(k0[j + 1], k1[j + 1], c[j + 1], nu[j + 1]);
         }
     };
     u32 ka = 0, ba = 0;
-    advance(ka, ba, wave);
+    if (per_wave) { ka = wave; ba = (u32)-1; advance(ka, ba, WSTRIDE); }
+    else advance(ka, ba, wave);
     u32 kb = ka, bb = ba;
     advance(kb, bb, WSTRIDE);
     v4u a0, a1, a2, b0, b1, b2;

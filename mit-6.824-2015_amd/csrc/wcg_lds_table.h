@@ -96,20 +96,27 @@ struct LdsTable {
             add_cnt(s < W ? p.b1 : p.b2, s % W, c);
             return true;
         }
-        while (e) {                             // insert: first empty slot of b1, then b2
-            const int s = __ffs(e) - 1;
-            e &= e - 1;
-            const u32 b = s < W ? p.b1 : p.b2;
-            const int j = s % W;
-            const u64 old = atomicCAS(&k0[b][j], 0ull, a0);
-            if (old == 0) {
-                if (!shrt) k1[b][j] = a1;
-                add_cnt(b, j, c);
-                return true;
+        // insert into the emptier of the two buckets first (two choices by load keep the buckets
+        // even; first-fit into b1 left enough full pairs at 40% load that 1.5% of pass-2 keys
+        // found both of their buckets full)
+        const u32 e1 = e & ((1u << W) - 1), e2 = e >> W;
+        const bool second = __popc(e2) > __popc(e1);
+        auto try_bucket = [&](u32 b, u32 m) -> bool {
+            while (m) {
+                const int j = __ffs(m) - 1;
+                m &= m - 1;
+                const u64 old = atomicCAS(&k0[b][j], 0ull, a0);
+                if (old == 0) {
+                    if (!shrt) k1[b][j] = a1;
+                    add_cnt(b, j, c);
+                    return true;
+                }
+                if (old == a0 && (shrt || k1[b][j] == a1)) { add_cnt(b, j, c); return true; }
             }
-            if (old == a0 && (shrt || k1[b][j] == a1)) { add_cnt(b, j, c); return true; }
-        }
-        return false;
+            return false;
+        };
+        if (second) return try_bucket(p.b2, e2) || try_bucket(p.b1, e1);
+        return try_bucket(p.b1, e1) || try_bucket(p.b2, e2);
     }
 
     __device__ __forceinline__ bool add(u64 a0, u64 a1, u32 h, CNT c) {
