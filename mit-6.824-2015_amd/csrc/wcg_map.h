@@ -57,6 +57,9 @@ constexpr int MAP_NM = 1024;                 // LDS medium-key slots (20 B each)
 #define WCG_MAP_SETS 4
 #endif
 constexpr int MAP_SETS = WCG_MAP_SETS;       // steps in flight per wave (2 or 4)
+#ifndef WCG_SHORT_PAIR
+#define WCG_SHORT_PAIR 0                     // 1: short-key iterations in pairs (two tokens per lane)
+#endif
 #ifndef WCG_MASKED_RESERVE
 #define WCG_MASKED_RESERVE 0                 // 1: miss reservations by the missing lanes only
 #endif
@@ -633,6 +636,9 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         bool missp = false;                   // the previous iteration's miss: bucket, units,
         u32 pp = 0, nup = 0, posp = 0;        // reservation and key
         u64 k0p = 0, k1p = 0;
+        bool missq = false;                   // paired short iterations: the second token's
+        u32 pq = 0, posq = 0;
+        u64 k0q = 0;
         const u32 rcap = (u32)a.region_cap;   // < 2^22 (host), so offsets fit 24-bit multiplies
         auto store_pending = [&](bool two) {
             const bool fits = missp && posp + nup <= rcap;
@@ -646,6 +652,18 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
                 ginsert(a.gtab, a.gmask, k0p, k1p, gslot(key_hash(k0p, k1p)), 1, a.st);
             }
         };
+        auto store_pending_q = [&]() {        // the paired loop's second pending short key
+            const bool fits = missq && posq + 1 <= rcap;
+            unit_store(prsrc, fits ? (__umul24(pq, rcap) + posq) * 8u : OOB, k0q);
+            if (missq && !fits) {
+                u64* r = wpool + (u64)pq * a.region_cap;
+                for (u32 k = posq; k < rcap; k++) r[k] = 0;
+                my_global++;
+                ginsert(a.gtab, a.gmask, k0q, 0, gslot(key_hash(k0q, 0)), 1, a.st);
+            }
+            missq = false;
+        };
+        u32 extra_stores = 0;
         // full iterations of short entries take the short body; the rest (the partial short
         // iteration, medium and long keys) the general one
         const u32 nsh = (ABL == 0 || ABL >= 6) ? (tot_s >> 6) : 0u;
@@ -677,9 +695,41 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
                 t.h = lds_hash32((u32)t.k, (u32)(t.k >> 32), 0u, 0u);
                 return t;
             };
-            TokS cs = decode_s(sst[lane], keyread_s(sst[lane]));
-            e_nxt = sst[64 + lane];
-            for (u32 it = 0; it < nsh; it++) {
+            u32 it = 0;
+#if WCG_SHORT_PAIR
+            // pairs of full short iterations: two tokens per lane, both probes and both next
+            // keys in one LDS round trip; each token's miss is stored one pair later (1 store per
+            // token, + 1 for the second pending slot after the loop)
+            if (nsh >= 2) {
+                TokS ca = decode_s(sst[lane], keyread_s(sst[lane]));
+                TokS cb = decode_s(sst[64 + lane], keyread_s(sst[64 + lane]));
+                u32 ea = sst[128 + lane], eb = sst[192 + lane];
+                for (; it + 2 <= nsh; it += 2) {
+                    const auto pa = tab.probe_short(ca.h);
+                    const auto pb = tab.probe_short(cb.h);
+                    const uint4 na = keyread_s(ea), nb = keyread_s(eb);
+                    const u32 ean = sst[(it + 4) * 64 + lane], ebn = sst[(it + 5) * 64 + lane];
+                    __builtin_amdgcn_sched_barrier(0);
+                    const bool ha = tab.finish_short(ca.k, ca.h, pa);
+                    const bool hb = tab.finish_short(cb.k, cb.h, pb);
+                    my_hits += (u32)ha + (u32)hb;
+                    store_pending(false);
+                    store_pending_q();
+                    missp = !ha; pp = miss_bucket(ca.h, a.pmask); nup = 1u; k0p = ca.k; k1p = 0;
+                    missq = !hb; pq = miss_bucket(cb.h, a.pmask); k0q = cb.k;
+                    posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
+                    posq = atomicAdd(&cursor[pq], missq ? 1u : 0u);
+                    ca = decode_s(ea, na);
+                    cb = decode_s(eb, nb);
+                    ea = ean; eb = ebn;
+                }
+                store_pending_q();
+                extra_stores = 1;
+            }
+#endif
+            TokS cs = decode_s(sst[it * 64 + lane], keyread_s(sst[it * 64 + lane]));
+            e_nxt = sst[(it + 1) * 64 + lane];
+            for (; it < nsh; it++) {
                 const auto pr = tab.probe_short(cs.h);
                 const uint4 nks = keyread_s(e_nxt);
                 const u32 e_nn = sst[(it + 2) * 64 + lane];
@@ -744,7 +794,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         if (ABL == 0 || ABL >= 6) store_pending(true);
         if (ABL) asm volatile("" ::"v"(sink));
         wave_lds_sync();
-        return (ABL == 0 || ABL >= 6) ? nsh + 2 * (iters + 1) : 0u;
+        return (ABL == 0 || ABL >= 6) ? nsh + 2 * (iters + 1) + extra_stores : 0u;
     };
 
     // ---- main loop, unrolled over the register sets so that each set's load and waits name
