@@ -18,8 +18,9 @@
 // Pass 2 (k_agg, mode AGG_EMIT): one workgroup per (p, q) sub-bucket aggregates it in LDS and emits
 // each distinct key as a record straight into the record log (no global-table insert); the
 // sub-buckets are disjoint, and keys also counted in the global table (pass-1 flushes) or emitted
-// by another map call are merged after the sort (wcg_sort.h: k_dd_*).  A full LDS table or a full
-// record log falls back to global-table inserts (exact either way).
+// by another map call are merged after the sort (wcg_sort.h: k_dd_merge).  An entry a full LDS
+// table cannot take is logged as a partial-count record (merged the same way); only a full record
+// log falls back to global-table inserts (exact either way).
 #pragma once
 #include "wcg_common.h"
 #include "wcg_lds_table.h"
@@ -33,6 +34,7 @@ constexpr int AGG_NB = 3350;           // 3350 x 2 slots x 24 B (u64 counts) = 1
 constexpr u32 AGG_SLACK_UNITS = AGG_BATCH + 8;   // pool tail slack for k_agg's unmasked loads
 constexpr u32 AGG_MAX_SRC = 256;       // source regions per workgroup (+1 KiB LDS = 160 KiB)
 constexpr u32 AGG_Q = 128;             // pass-2 sub-buckets per bucket
+constexpr u32 AGG_OVF_CAP = 4096;      // pass 2: overflow records staged per workgroup (128 KiB)
 constexpr int AGG_SPILL = 0, AGG_EMIT = 1;
 
 struct AggArgs {
@@ -57,23 +59,9 @@ struct AggArgs {
     u32* spill_len;
     Rec* emit;             // pass 2: record log (emit_cap records; st->nemit used)
     u64 emit_cap;
+    Rec* ovf;              // pass 2: per-workgroup staging of the entries a full LDS table
+    u32 ovf_cap;           //   cannot take (ovf_cap records per workgroup)
 };
-
-// the record of an inline key (k0, k1) of fact F4 (the same conversion as k_compact's)
-__device__ __forceinline__ Rec inline_rec(u64 k0, u64 k1, u64 cnt) {
-    Rec r;
-    if (key_short(k0)) {
-        r.hi = bswap64(k0 & 0x00FFFFFFFFFFFFFFull);
-        r.lo = 0;
-        r.ref = k0 >> 56;
-    } else {
-        r.hi = bswap64(k0);
-        r.lo = bswap64(k1 & 0x00FFFFFFFFFFFFFFull);
-        r.ref = k1 >> 56;
-    }
-    r.cnt = cnt;
-    return r;
-}
 
 // bucket choices of pass 2's tables: the high half of the 64-bit key hash (a sub-bucket's keys
 // share 13 bits of the 32-bit LDS hash, which pass 1 uses: it is cheaper and its keys vary in all
@@ -136,10 +124,16 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
     __syncthreads();
     u64 my_global = 0;
     u64* const sp = emit ? nullptr : a.spill + (u64)bi * a.spill_cap;
-    // count c of (k0, k1) the table could not take: pass 1 spills the entry, pass 2 (and a full
-    // spill region) inserts it into the global table
+    // count c of (k0, k1) the table could not take: pass 1 spills the entry; pass 2 stages it as a
+    // partial-count record (appended to the record log with the table's records, the duplicates
+    // merged after the sort as for keys emitted by several map calls), so that the global table
+    // stays empty and compaction skips its scan; a full spill region or staging area inserts it
+    // into the global table
     auto overflow = [&](u64 k0, u64 k1, u64 c, u32 nu) {
-        if (!emit) {
+        if (emit) {
+            const u32 pos = atomicAdd(&spos, 1u);
+            if (pos < a.ovf_cap) { a.ovf[(u64)blockIdx.x * a.ovf_cap + pos] = inline_rec(k0, k1, c); return; }
+        } else {
             const u32 pos = atomicAdd(&spos, nu);
             if (pos + nu <= a.spill_cap) {
                 u64 e[3];
@@ -256,9 +250,22 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
         __syncthreads();
         u32 pre = 0, all = 0;
         for (int w = 0; w < AGG_NT / 64; w++) { if (w < wave) pre += (u32)wsum[w][0]; all += (u32)wsum[w][0]; }
-        if (tid == 0) wsum[0][1] = all ? atomicAdd((unsigned long long*)&a.st->nemit, (unsigned long long)all) : 0;
+        const u32 nov = spos < a.ovf_cap ? spos : a.ovf_cap;       // staged overflow records
+        if (tid == 0)
+            wsum[0][1] = all + nov ? atomicAdd((unsigned long long*)&a.st->nemit, (unsigned long long)(all + nov)) : 0;
         __syncthreads();
-        u64 pos = wsum[0][1] + pre + incl - mine;
+        const u64 base = wsum[0][1];
+        for (u32 i = tid; i < nov; i += AGG_NT) {                    // after the table's records
+            const Rec r = a.ovf[(u64)blockIdx.x * a.ovf_cap + i];
+            if (base + all + i < a.emit_cap) a.emit[base + all + i] = r;
+            else {
+                my_global++;
+                u64 k0, k1;
+                rec_inline_key(r, k0, k1);
+                ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), r.cnt, a.st);
+            }
+        }
+        u64 pos = base + pre + incl - mine;
         for (int i = tid; i < AGG_NB * AGG_W; i += AGG_NT) {
             const u64 c = (&tcnt[0][0])[i];
             if (!c) continue;

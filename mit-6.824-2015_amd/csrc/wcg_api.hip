@@ -58,6 +58,7 @@ struct wcg_ctx {
     u64* pool2 = nullptr; u64 pool2_cap = 0;  // k_rp sub-bucket regions
     u32* rlen2 = nullptr; u64 rlen2_cap = 0;
     Rec* remit = nullptr; u64 remit_cap = 0;  // record log of k_agg's pass 2
+    Rec* ovf = nullptr; u64 ovf_cap = 0;      // pass 2's per-workgroup overflow staging
     bool two_pass_used = false;               // a map call since wcg_reset ran the two passes
     bool imported = false;                    // wcg_import since wcg_reset
     u32* lpcur = nullptr; u64 lpcur_cap = 0;    // 2n records: by bucket, and the oversized-bucket scratch
@@ -93,7 +94,7 @@ struct wcg_ctx {
     // long-token log (k_map -> k_long): one region of {offset | len << 40} records per workgroup
     u64* llog = nullptr; u64 llog_cap = 0;
     u32* llog_len = nullptr; u64 llog_len_cap = 0;
-    u32 nbuckets = 64;
+    u32 nbuckets = 64;                                // miss buckets P (<= MAX_MISS_BUCKETS)
     // ingest (wcg_ingest.h): two pinned staging buffers, two device buffers, a reader pool
     u64 chunk = 64ull << 20;
     uint8_t* hb[2] = {nullptr, nullptr};
@@ -610,7 +611,7 @@ int wcg_close(wcg_ctx* c) {
     }
     void* bufs[] = {c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens, c->d_scalar, c->d_out,
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
-                    c->llog, c->llog_len, c->smp, c->bid, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->hist, c->spart, c->ikey, c->iidx, c->groups,
+                    c->llog, c->llog_len, c->smp, c->bid, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->ovf, c->hist, c->spart, c->ikey, c->iidx, c->groups,
                     c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);
@@ -681,6 +682,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // high-cardinality UTF-8 text (C4: 0.1 tokens per byte, 79% misses, 2-unit keys), where a
     // 1-per-8 pool overflowed into per-token global-table inserts; only written units cost time
     const u32 P = c->nbuckets;
+    static_assert(MAX_MISS_BUCKETS >= 64, "k_map's LDS cursors cover the 64 miss buckets");
     u64 per_wg_bytes = (u64)a.tiles_per_wg * MAP_STEP;
     // even (16-byte aligned regions); a workgroup's regions stay under 2 GiB so k_map's unit
     // offsets fit 32 bits and its 24-bit multiplies (P * region_cap * 8 <= 2^31)
@@ -729,6 +731,17 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     }
     a.llog = c->llog;
     a.llog_len = c->llog_len;
+    // Two passes only for high-cardinality jobs (the table is sized for more than 4M keys, or
+    // WCG_AGG_TWO_PASS=1): on low-cardinality text nothing spills, and the extra launches and the
+    // record-log merge would only cost time.  One pass sends an entry its LDS table cannot take
+    // to the global table.  Two-pass jobs keep the global table empty: pass 2's records, its
+    // overflow and k_long_hash's inline runs all go to the record log.
+    static const char* tp_env = getenv("WCG_AGG_TWO_PASS");
+    const bool two_pass = tp_env ? atoi(tp_env) != 0 : c->max_keys > (4ull << 20);
+    const u64 rec_cap_emit = c->max_keys + 65536;
+    RC(ensure(c, &c->remit, &c->remit_cap, rec_cap_emit));
+    a.emit = two_pass ? c->remit : nullptr;
+    a.emit_cap = rec_cap_emit;
     a.pool = c->pool;
     a.region_len = c->region_len;
     a.wg_stats = c->wg_stats;
@@ -773,20 +786,13 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g.gtab = c->gtab; g.gmask = c->gslots - 1; g.st = c->st;
     g.map_stats = c->wg_stats;
     const u32 nb1 = P * g.slices;
-    // Two passes only for high-cardinality jobs (the table is sized for more than 4M keys, or
-    // WCG_AGG_TWO_PASS=1): on low-cardinality text nothing spills, and the extra launches and the
-    // record-log merge would only cost time.  One pass sends an entry its LDS table cannot take
-    // to the global table.
-    static const char* tp_env = getenv("WCG_AGG_TWO_PASS");
-    const bool two_pass = tp_env ? atoi(tp_env) != 0 : c->max_keys > (4ull << 20);
     // a workgroup spills at most what it reads: its slice's regions
     g.spill_cap = two_pass ? (u64)cdiv(grid, g.slices) * a.region_cap : 0;
     RC(ensure(c, &c->spill, &c->spill_cap, std::max<u64>(nb1 * g.spill_cap, 1)));
     RC(ensure(c, &c->spill_len, &c->spill_len_cap, (u64)nb1));
     g.spill = c->spill; g.spill_len = c->spill_len;
-    const u64 rec_cap_emit = c->max_keys + 65536;
-    RC(ensure(c, &c->remit, &c->remit_cap, rec_cap_emit));
     g.emit = c->remit; g.emit_cap = rec_cap_emit;
+    g.ovf = nullptr; g.ovf_cap = 0;
     k_agg<<<nb1, AGG_NT, 0, c->stream>>>(g);
     HIPCHK(c, hipGetLastError());
     if (two_pass) {
@@ -802,7 +808,11 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g2.pool = c->pool2; g2.region_len = c->rlen2; g2.region_cap = cap2;
     g2.P = P * AGG_Q; g2.nsrc = g.slices; g2.slices = 1;
     g2.rstride = AGG_Q; g2.rmod = AGG_Q; g2.P1 = P; g2.mode = AGG_EMIT;
-    k_agg<<<std::min<u32>(P * AGG_Q, (u32)c->ncu * 2), AGG_NT, 0, c->stream>>>(g2);
+    const u32 grid2 = std::min<u32>(P * AGG_Q, (u32)c->ncu * 2);
+    g2.ovf_cap = AGG_OVF_CAP;
+    RC(ensure(c, &c->ovf, &c->ovf_cap, (u64)grid2 * AGG_OVF_CAP));
+    g2.ovf = c->ovf;
+    k_agg<<<grid2, AGG_NT, 0, c->stream>>>(g2);
     HIPCHK(c, hipGetLastError());
     }
     if (c->timing) {

@@ -165,12 +165,37 @@ __device__ __forceinline__ bool nonascii_letter(u32 cp) {
     return lt_is_letter(cp);
 }
 
+// k_map's copy of the letter table in LDS.  A load from the global table would be followed by
+// s_waitcnt vmcnt(0), which also waits for every window prefetch in flight (vmcnt counts all
+// older loads): on mixed UTF-8 text that drained k_map's prefetch pipeline almost every step.
+// Blocks 0-7 (U+0000-07FF) are table blocks 0-7, so 2-byte runes need no index read.
+constexpr u32 LT_LDS_BLOCKS = 0x314;          // 256-code-point blocks up to the last letter (U+3134A)
+struct LdsLetters {
+    const uint8_t* idx;                       // [LT_LDS_BLOCKS + 1]: block ids; the last is empty
+    const u32* bits;                          // [WCG_LT_NBLOCKS * 8]
+};
+__device__ __forceinline__ bool nonascii_letter_lds(u32 cp, LdsLetters t) {
+    if ((cp - 0x4E00u) <= 0x9FFCu - 0x4E00u || (cp - 0xAC00u) <= 0xD7A3u - 0xAC00u ||
+        (cp - 0x3400u) <= 0x4DBFu - 0x3400u || (cp - 0x20000u) <= 0x2A6DDu - 0x20000u)
+        return true;
+    const u32 b = cp >> 8;
+    const u32 blk = b < 8 ? b : t.idx[b < LT_LDS_BLOCKS ? b : LT_LDS_BLOCKS];
+    return (t.bits[blk * 8 + ((cp >> 5) & 7)] >> (cp & 31)) & 1u;
+}
+// fill the LDS copy (all threads of the workgroup; a barrier must follow)
+__device__ __forceinline__ void lds_letters_init(uint8_t* idx, u32* bits, int tid, int nt) {
+    for (int i = tid; i <= (int)LT_LDS_BLOCKS; i += nt)
+        idx[i] = WCG_LT_STAGE1[i < (int)LT_LDS_BLOCKS ? i : 0x10FF];
+    for (int i = tid; i < WCG_LT_NBLOCKS * 8; i += nt) bits[i] = WCG_LT_STAGE2[i >> 3][i & 7];
+}
+
 // 16-bit letter mask of a chunk containing non-ASCII bytes, decoded from registers (fact F1):
 // `c` = the chunk, `pw` = the last 4 bytes before it, `nx` = the first 4 bytes after it (zeros
 // outside the input or the window).  Every non-continuation byte in [-3, 16) starts a rune in
 // Go's decoding; a valid letter rune marks all its bytes; every other byte is a non-letter
 // (utf8.RuneError, width 1).  Fully unrolled: each byte is a constant bit-field of six dwords.
-__device__ __forceinline__ u32 utf8_mask_regs(uint4 c, u32 pw, u32 nx) {
+// Letter tests read the LDS copy `lt` of the table (nonascii_letter_lds).
+__device__ __forceinline__ u32 utf8_mask_regs(uint4 c, u32 pw, u32 nx, LdsLetters lt) {
     const u32 d[6] = {pw, c.x, c.y, c.z, c.w, nx};
     // ASCII letters of the chunk (high-bit bytes masked off, then dropped)
     u32 m = (ascii_mask4(c.x & 0x7F7F7F7Fu) & ~high_mask4(c.x)) |
@@ -191,7 +216,7 @@ __device__ __forceinline__ u32 utf8_mask_regs(uint4 c, u32 pw, u32 nx) {
             const u32 cp = w == 2 ? ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu)
                          : w == 3 ? ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu)
                                   : ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
-            if (ok && nonascii_letter(cp)) {
+            if (ok && nonascii_letter_lds(cp, lt)) {
                 const u32 span = (1u << w) - 1u;
                 m |= i >= 0 ? span << i : span >> (-i);
             }
@@ -226,6 +251,27 @@ __device__ __forceinline__ u32 lds_hash(u64 k0, u64 k1) {
 __device__ __forceinline__ u32 fnv1a_step(u32 h, u32 byte) { return (h ^ byte) * 0x01000193u; }
 
 __device__ __forceinline__ u64 bswap64(u64 x) { return __builtin_bswap64(x); }
+
+// the record of an inline key (k0, k1) of fact F4 (the same conversion as k_compact's)
+__device__ __forceinline__ Rec inline_rec(u64 k0, u64 k1, u64 cnt) {
+    Rec r;
+    if (key_short(k0)) {
+        r.hi = bswap64(k0 & 0x00FFFFFFFFFFFFFFull);
+        r.lo = 0;
+        r.ref = k0 >> 56;
+    } else {
+        r.hi = bswap64(k0);
+        r.lo = bswap64(k1 & 0x00FFFFFFFFFFFFFFull);
+        r.ref = k1 >> 56;
+    }
+    r.cnt = cnt;
+    return r;
+}
+// ... and back (ref = the key's length, < 16)
+__device__ __forceinline__ void rec_inline_key(const Rec& r, u64& k0, u64& k1) {
+    if (r.ref < 8) { k0 = bswap64(r.hi) | r.ref << 56; k1 = 0; }
+    else { k0 = bswap64(r.hi); k1 = bswap64(r.lo) | r.ref << 56; }
+}
 
 // mask keeping the low `nbytes` bytes (0..8)
 __device__ __forceinline__ u64 low_bytes_mask(int nbytes) {

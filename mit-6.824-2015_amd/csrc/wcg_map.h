@@ -50,8 +50,9 @@ constexpr int MAP_SST = 512;                 // max token starts per step (992 /
 #ifndef WCG_ADMIT2
 #define WCG_ADMIT2 1                         // k_map LDS tables admit keys on their second miss
 #endif
-constexpr int MAP_NS = WCG_ADMIT2 ? 8704 : 8896;   // LDS short-key slots (12 B each; the 2 KiB
-                                                  // admission filter takes 192 of them)
+constexpr int MAP_NS = WCG_ADMIT2 ? 8432 : 8624;   // LDS short-key slots (12 B each; the 2 KiB
+                                                  // admission filter takes 192 of them, the
+                                                  // LDS letter table 4.3 KiB)
 constexpr int MAP_NM = 1024;                 // LDS medium-key slots (20 B each)
 #ifndef WCG_MAP_SETS
 #define WCG_MAP_SETS 4
@@ -69,7 +70,7 @@ constexpr int MAP_SETS = WCG_MAP_SETS;       // steps in flight per wave (2 or 4
 #ifndef WCG_NOWAIT
 #define WCG_NOWAIT 0                         // diagnostics: 1 = never wait for the window loads
 #endif
-constexpr int MAX_MISS_BUCKETS = 256;
+constexpr int MAX_MISS_BUCKETS = 64;         // miss buckets P (the host uses 64)
 constexpr u32 SST_LEN_SHIFT = 10;            // start entry = window offset | min(run, 16) << 10
 
 struct MapArgs {
@@ -87,6 +88,7 @@ struct MapArgs {
     u64* wg_stats;                 // [grid][4] per-workgroup {tokens, lds hits, global ops, long}
     u64* llog;     u32 llog_cap;    // long-token log: region wg = llog[wg * llog_cap ...]
     u32* llog_len;                 // records written per region
+    Rec* emit;     u64 emit_cap;    // two-pass jobs: the record log (k_long_hash's inline runs)
 };
 constexpr u64 LLOG_OFF_MASK = (1ull << 40) - 1;   // record = input offset | len << 40 (len 0: walk)
 constexpr u32 LLOG_PER_STEP = 64;                 // long-token log records per step: a bound (a
@@ -214,7 +216,8 @@ __device__ u64 long_walk(const MapArgs& a, u64 p, u64* hash) {
     return q - p;
 }
 
-// a run that turned out to be an inline key (<= 15 bytes: measured only after a rune walk)
+// a run that turned out to be an inline key (<= 15 bytes: measured only after a rune walk); called
+// by the lanes of a wave that found one
 __device__ __forceinline__ void count_inline_run(const MapArgs& a, u64 p, u64 len) {
     u64 b0 = 0, b1 = 0;
     for (u64 i = 0; i < len; i++) {
@@ -223,7 +226,16 @@ __device__ __forceinline__ void count_inline_run(const MapArgs& a, u64 p, u64 le
     }
     u64 k0, k1;
     make_key(b0, b1, (int)len, k0, k1);
+    if (a.emit) {                     // two-pass job: one record in the record log (merged after
+        const u64 act = __ballot(1);  // the sort), one atomic per wave: the global table stays empty
+        const u32 rank = __builtin_amdgcn_mbcnt_hi((u32)(act >> 32), __builtin_amdgcn_mbcnt_lo((u32)act, 0u));
+        u64 base = 0;
+        if (rank == 0) base = atomicAdd((unsigned long long*)&a.st->nemit, (unsigned long long)__popcll(act));
+        base = (u64)__builtin_amdgcn_readfirstlane((u32)(base >> 32)) << 32 | __builtin_amdgcn_readfirstlane((u32)base);
+        if (base + rank < a.emit_cap) { a.emit[base + rank] = inline_rec(k0, k1, 1); return; }
+    }
     ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), 1, a.st);
+    atomicAdd(&a.st->global_ops, 1ull);
 }
 
 // key word j (little-endian bytes 4j..4j+3 of the key at input offset p, zeros past len) from
@@ -326,7 +338,7 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
         u64 len = r >> 40, h = 0;
         if (i < nrec && len == 0) {
             len = long_walk(a, p, &h);
-            if (len <= 15) { count_inline_run(a, p, len); atomicAdd(&a.st->global_ops, 1ull); len = 0; }
+            if (len <= 15) { count_inline_run(a, p, len); len = 0; }
             else if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); len = 0; }
         } else if (len != 0) {
             h = 0xCBF29CE484222325ull;
@@ -491,6 +503,8 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     __shared__ u32 mcnt[MAP_NM];
     __shared__ u32 cursor[MAX_MISS_BUCKETS];
     __shared__ u32 lcur;                        // long-token log cursor
+    __shared__ uint8_t lt_idx[LT_LDS_BLOCKS + 4];   // letter table (UTF-8 chunks)
+    __shared__ u32 lt_bits[WCG_LT_NBLOCKS * 8];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);     // wave-uniform (scalar)
@@ -498,7 +512,9 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     tab.init(tid, MAP_NT);
     for (int i = tid; i < MAX_MISS_BUCKETS; i += MAP_NT) cursor[i] = 0;
     if (tid == 0) lcur = 0;
+    lds_letters_init(lt_idx, lt_bits, tid, MAP_NT);
     __syncthreads();
+    const LdsLetters lt{lt_idx, lt_bits};
 
     uint8_t* const bytes = wbytes[wave];
     uint16_t* const sst = wstart[wave];
@@ -581,7 +597,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         if (all_ascii(mine)) {
             m = ascii_mask16(mine);
         } else {
-            m = utf8_mask_regs(mine, pw, nx);
+            m = utf8_mask_regs(mine, pw, nx, lt);
             if (lane == 63) m |= 0xE000u;
         }
         if (ABL == 4) { asm volatile("" ::"v"(m)); return 0; }
