@@ -154,17 +154,6 @@ __device__ __forceinline__ u32 high_mask4(u32 x) {
     return ((((x & 0x80808080u) >> 7) * 0x00204081u) >> 21) & 0xFu;
 }
 
-// Letter test of a validly decoded non-ASCII code point.  The four largest all-letter blocks of
-// Unicode 13.0 (CJK Ext A 3400-4DBF, CJK 4E00-9FFC, Hangul AC00-D7A3, CJK Ext B 20000-2A6DD:
-// 62% of all letters; tests/test_oracle.py checks them against unicodedata 13.0) answer
-// from registers; every other code point reads the two-level table.
-__device__ __forceinline__ bool nonascii_letter(u32 cp) {
-    if ((cp - 0x4E00u) <= 0x9FFCu - 0x4E00u || (cp - 0xAC00u) <= 0xD7A3u - 0xAC00u ||
-        (cp - 0x3400u) <= 0x4DBFu - 0x3400u || (cp - 0x20000u) <= 0x2A6DDu - 0x20000u)
-        return true;
-    return lt_is_letter(cp);
-}
-
 // k_map's copy of the letter table in LDS.  A load from the global table would be followed by
 // s_waitcnt vmcnt(0), which also waits for every window prefetch in flight (vmcnt counts all
 // older loads): on mixed UTF-8 text that drained k_map's prefetch pipeline almost every step.
@@ -174,14 +163,6 @@ struct LdsLetters {
     const uint8_t* idx;                       // [LT_LDS_BLOCKS + 1]: block ids; the last is empty
     const u32* bits;                          // [WCG_LT_NBLOCKS * 8]
 };
-__device__ __forceinline__ bool nonascii_letter_lds(u32 cp, LdsLetters t) {
-    if ((cp - 0x4E00u) <= 0x9FFCu - 0x4E00u || (cp - 0xAC00u) <= 0xD7A3u - 0xAC00u ||
-        (cp - 0x3400u) <= 0x4DBFu - 0x3400u || (cp - 0x20000u) <= 0x2A6DDu - 0x20000u)
-        return true;
-    const u32 b = cp >> 8;
-    const u32 blk = b < 8 ? b : t.idx[b < LT_LDS_BLOCKS ? b : LT_LDS_BLOCKS];
-    return (t.bits[blk * 8 + ((cp >> 5) & 7)] >> (cp & 31)) & 1u;
-}
 // fill the LDS copy (all threads of the workgroup; a barrier must follow)
 __device__ __forceinline__ void lds_letters_init(uint8_t* idx, u32* bits, int tid, int nt) {
     for (int i = tid; i <= (int)LT_LDS_BLOCKS; i += nt)
@@ -189,41 +170,81 @@ __device__ __forceinline__ void lds_letters_init(uint8_t* idx, u32* bits, int ti
     for (int i = tid; i < WCG_LT_NBLOCKS * 8; i += nt) bits[i] = WCG_LT_STAGE2[i >> 3][i & 7];
 }
 
-// 16-bit letter mask of a chunk containing non-ASCII bytes, decoded from registers (fact F1):
-// `c` = the chunk, `pw` = the last 4 bytes before it, `nx` = the first 4 bytes after it (zeros
-// outside the input or the window).  Every non-continuation byte in [-3, 16) starts a rune in
-// Go's decoding; a valid letter rune marks all its bytes; every other byte is a non-letter
-// (utf8.RuneError, width 1).  Fully unrolled: each byte is a constant bit-field of six dwords.
-// Letter tests read the LDS copy `lt` of the table (nonascii_letter_lds).
-__device__ __forceinline__ u32 utf8_mask_regs(uint4 c, u32 pw, u32 nx, LdsLetters lt) {
-    const u32 d[6] = {pw, c.x, c.y, c.z, c.w, nx};
-    // ASCII letters of the chunk (high-bit bytes masked off, then dropped)
+// 4 bytes -> 4-bit mask of the continuation bytes (80-BF)
+__device__ __forceinline__ u32 cont_mask4(u32 x) {
+    const u32 t = (x & 0xC0C0C0C0u) ^ 0x80808080u;          // zero bytes = continuation bytes
+    const u32 c = ~(t | (t << 1)) & 0x80808080u;
+    return (((c >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+// 19-bit letter mask of a chunk containing non-ASCII bytes (fact F1).  Bits 0-15: the chunk's
+// ASCII letters and the bytes of the letter runes that START in the chunk; bits 16-18: bytes of
+// the next chunk covered by such a rune.  The caller ORs the predecessor chunk's bits 16-18 into
+// bits 0-2 (one DPP lane shift), which replaces decoding three look-back positions per chunk.
+// `nx` = the first 4 bytes after the chunk (zeros outside the input or the window).
+// Branch-free over the 16 positions: every non-ASCII lead decodes (Go's utf8.DecodeRune: the
+// continuation bytes, then the code point's range, which rules out exactly what the E0/ED/F0/F4
+// second-byte rules reject - overlong forms, surrogates and > U+10FFFF); a position that is not
+// a valid lead gets cp 0.  The LDS table reads of a group of positions issue back to back and
+// complete under one wait.  (A branch per position ran the whole decode for every position any
+// lane needed, with two dependent LDS round trips each: 2.5 ms per GiB of C4 text.)
+#ifndef WCG_UTF8_GROUP
+#define WCG_UTF8_GROUP 8
+#endif
+__device__ __forceinline__ u32 utf8_mask_lds(uint4 c, u32 nx, LdsLetters lt) {
+    const u32 d[5] = {c.x, c.y, c.z, c.w, nx};
     u32 m = (ascii_mask4(c.x & 0x7F7F7F7Fu) & ~high_mask4(c.x)) |
             ((ascii_mask4(c.y & 0x7F7F7F7Fu) & ~high_mask4(c.y)) << 4) |
             ((ascii_mask4(c.z & 0x7F7F7F7Fu) & ~high_mask4(c.z)) << 8) |
             ((ascii_mask4(c.w & 0x7F7F7F7Fu) & ~high_mask4(c.w)) << 12);
-#define WCG_B(j) ((d[((j) + 4) >> 2] >> (8 * (((j) + 4) & 3))) & 0xFFu)
+    const u32 cont = cont_mask4(c.x) | (cont_mask4(c.y) << 4) | (cont_mask4(c.z) << 8) |
+                     (cont_mask4(c.w) << 12) | (cont_mask4(nx) << 16);   // bit j: byte j
+    constexpr int G = WCG_UTF8_GROUP;
 #pragma unroll
-    for (int i = -3; i < 16; i++) {
-        const u32 b0 = WCG_B(i);
-        if (b0 - 0xC2u <= 0xF4u - 0xC2u) {                 // a multi-byte lead (C2-F4)
-            const u32 b1 = WCG_B(i + 1), b2 = WCG_B(i + 2), b3 = WCG_B(i + 3);
-            const u32 w = b0 < 0xE0u ? 2u : (b0 < 0xF0u ? 3u : 4u);
-            const u32 lo = b0 == 0xE0u ? 0xA0u : (b0 == 0xF0u ? 0x90u : 0x80u);
-            const u32 hi = b0 == 0xEDu ? 0x9Fu : (b0 == 0xF4u ? 0x8Fu : 0xBFu);
-            const bool ok = b1 >= lo && b1 <= hi && (w < 3 || (b2 & 0xC0u) == 0x80u) &&
-                            (w < 4 || (b3 & 0xC0u) == 0x80u);
-            const u32 cp = w == 2 ? ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu)
-                         : w == 3 ? ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu)
-                                  : ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
-            if (ok && nonascii_letter_lds(cp, lt)) {
-                const u32 span = (1u << w) - 1u;
-                m |= i >= 0 ? span << i : span >> (-i);
-            }
+    for (int k0 = 0; k0 < 16; k0 += G) {
+        u32 cp[G], span[G], blk[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int i = k0 + g;
+            const u32 wd = (i & 3) ? __builtin_amdgcn_alignbyte(d[(i >> 2) + 1], d[i >> 2], i & 3) : d[i >> 2];
+            // arithmetic forms only (no selects between literals: each literal a select needs
+            // would be held in a VGPR across k_map's token loops)
+            const u32 b0 = wd & 0xFFu;
+            const bool lead = b0 - 0xC2u <= 0xF4u - 0xC2u;
+            const u32 w = __builtin_clz(~(wd << 24));          // leading ones of b0: 2-4 for a lead
+            const u32 need = (1u << ((w - 1) & 31)) - 1u;      // continuation bytes 1..w-1
+            const bool conts = ((cont >> (i + 1)) & need) == need;
+            const u32 x = ((b0 & (0x7Fu >> (w & 31))) << 18) | ((wd << 4) & 0x3F000u) | ((wd >> 10) & 0xFC0u) |
+                          ((wd >> 24) & 0x3Fu);
+            const u32 v = x >> ((24 - 6 * w) & 31);
+            // overlong (3 bytes: < U+0800, 4 bytes: < U+10000; 2 bytes: C2-DF never are),
+            // surrogates, > U+10FFFF
+            const bool ok = lead & conts & ((v >> ((5 * w - 4) & 31)) != 0u) & (v - 0xD800u >= 0x800u) &
+                            (v <= 0x10FFFFu);
+            cp[g] = ok ? v : 0u;                               // cp 0: not a letter
+            span[g] = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0, w & 31) << i;   // w bytes from i
         }
+        // the reads of a group issue before any of their uses (the scheduler otherwise waited
+        // for each read in turn)
+        u32 t[G], bits[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const u32 b = cp[g] >> 8;
+            t[g] = lt.idx[b < LT_LDS_BLOCKS ? b : LT_LDS_BLOCKS];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const u32 b = cp[g] >> 8;
+            blk[g] = b < 8 ? b : t[g];
+            bits[g] = lt.bits[blk[g] * 8 + ((cp[g] >> 5) & 7)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < G; g++) m |= ((bits[g] >> (cp[g] & 31)) & 1u) ? span[g] : 0u;
+        __builtin_amdgcn_sched_barrier(0);           // groups stay apart (register pressure)
     }
-#undef WCG_B
-    return m & 0xFFFFu;
+    return m;
 }
 
 // ------------------------------------------------------------------ hashing

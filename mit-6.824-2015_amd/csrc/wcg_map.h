@@ -590,16 +590,17 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         //      the step's first byte; lane 63: only as the successor of chunk 62, and on the
         //      UTF-8 path its last 3 bits, whose runes may end past the window, are forced to
         //      letters, so a run reaching them is measured exactly by the long-token path)
-        // the neighbour chunks' edge dwords by DPP (all lanes active; lane 0 / 63 get zeros)
-        const u32 pw = (u32)__builtin_amdgcn_update_dpp(0, (int)mine.w, 0x138, 0xF, 0xF, false);   // wave_shr:1
+        // the next chunk's first dword by DPP (all lanes active; lane 63 gets zeros)
         const u32 nx = (u32)__builtin_amdgcn_update_dpp(0, (int)mine.x, 0x130, 0xF, 0xF, false);   // wave_shl:1
         u32 m;
         if (all_ascii(mine)) {
             m = ascii_mask16(mine);
         } else {
-            m = utf8_mask_regs(mine, pw, nx, lt);
+            m = utf8_mask_lds(mine, nx, lt);
             if (lane == 63) m |= 0xE000u;
         }
+        // bytes of this chunk covered by a letter rune that started in the previous chunk
+        m = (m | ((u32)__builtin_amdgcn_update_dpp(0, (int)(m >> 16), 0x138, 0xF, 0xF, false) & 7u)) & 0xFFFFu;
         if (ABL == 4) { asm volatile("" ::"v"(m)); return 0; }
         wmask[wave][lane] = (uint16_t)m;
         // neighbours' masks by DPP lane shifts
