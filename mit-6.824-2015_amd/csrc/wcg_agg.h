@@ -18,7 +18,7 @@
 // Pass 2 (k_agg, mode AGG_EMIT): one workgroup per (p, q) sub-bucket aggregates it in LDS and emits
 // each distinct key as a record straight into the record log (no global-table insert); the
 // sub-buckets are disjoint, and keys also counted in the global table (pass-1 flushes) or emitted
-// by another map call are merged after the sort (wcg_sort.h: k_dd_merge).  An entry a full LDS
+// by another map call are merged by the bucket sort (wcg_sort.h: dd_same).  An entry a full LDS
 // table cannot take is logged as a partial-count record (merged the same way); only a full record
 // log falls back to global-table inserts (exact either way).
 #pragma once

@@ -60,6 +60,7 @@ struct wcg_ctx {
     Rec* remit = nullptr; u64 remit_cap = 0;  // record log of k_agg's pass 2
     Rec* ovf = nullptr; u64 ovf_cap = 0;      // pass 2's per-workgroup overflow staging
     bool two_pass_used = false;               // a map call since wcg_reset ran the two passes
+    bool gtab_zero = false;                   // the global table was cleared by the last wcg_reset
     bool imported = false;                    // wcg_import since wcg_reset
     u32* lpcur = nullptr; u64 lpcur_cap = 0;    // 2n records: by bucket, and the oversized-bucket scratch
     u32* hist = nullptr; u64 hist_cap = 0;    // [B][G] bucket counts / partition counts
@@ -334,6 +335,11 @@ int sort_records(wcg_ctx* c) {
     target = std::max<u64>(target, cdiv(n, SS_MAXB));
     SortArgs a;
     a.rec = c->recA; a.n = n; a.out = c->recB;
+    // the record log: a key may repeat (the global table, other map calls, pass 2's overflow):
+    // the bucket sort merges the copies and counts the distinct keys
+    a.dedupe = c->h_st->nemit != 0;
+    a.nkeys = c->d_scalar + 8;                     // its own slot (the scans use d_scalar[0])
+    if (a.dedupe) HIPCHK(c, hipMemsetAsync(a.nkeys, 0, sizeof(u64), c->stream));
     a.B = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, target), SS_MAXB));
     a.S = a.B > 1 ? std::min<u64>(n, (u64)a.B * SS_OVS) : 0;
     a.smp = nullptr;
@@ -372,14 +378,9 @@ int sort_records(wcg_ctx* c) {
     if (getenv("WCG_DEBUG"))
         fprintf(stderr, "wcg: nemit %llu global_ops %llu\n", (unsigned long long)c->h_st->nemit,
                 (unsigned long long)c->h_st->global_ops);
-    // the record log: a key may repeat (the global table, other map calls, racing inserts of one
-    // key in pass 2): duplicates merged in place (k_dd_merge, wcg_sort.h)
     c->nkeys = n;
-    if (c->h_st->nemit) {
-        HIPCHK(c, hipMemsetAsync(c->d_scalar, 0, sizeof(u64), c->stream));
-        k_dd_merge<<<grid_for(n, 256, c->ncu * 8), 256, 0, c->stream>>>(c->recB, n, c->d_scalar);
-        HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    if (a.dedupe) {
+        HIPCHK(c, hipMemcpyAsync(c->h_scalar, a.nkeys, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         c->nkeys = *c->h_scalar;
     }
@@ -640,7 +641,17 @@ int wcg_reset(wcg_ctx* c) {
     if (!c) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
-    HIPCHK(c, hipMemsetAsync(c->gtab, 0, c->gslots * sizeof(GEntry), c->stream));
+    // The global table (up to GBs) is cleared only if something may have written it since it was
+    // last cleared: every kernel that inserts into it counts global_ops, and wcg_import sets
+    // `imported`; two-pass jobs normally leave it empty.
+    bool clear_g = true;
+    if (c->gtab_zero && !c->imported) {
+        HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        clear_g = c->h_st->global_ops != 0;
+    }
+    if (clear_g) HIPCHK(c, hipMemsetAsync(c->gtab, 0, c->gslots * sizeof(GEntry), c->stream));
+    c->gtab_zero = true;
     HIPCHK(c, hipMemsetAsync(c->ltab, 0, c->lslots * sizeof(GEntry), c->stream));
     HIPCHK(c, hipMemsetAsync(c->st, 0, sizeof(DevState), c->stream));
     c->compacted = c->reduced = false;

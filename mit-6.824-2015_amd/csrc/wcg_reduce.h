@@ -140,7 +140,7 @@ __device__ u32 rec_ihash(const Rec& r, const uint8_t* arena) {
 constexpr int FMT_MERGED = 0, FMT_JSON = 1, FMT_JSON_ALL = 2, FMT_COPY = 3;
 constexpr u64 JSON_FIXED = 8 + 11 + 3;   // {"Key":" + ","Value":" + "}\n
 
-// a record with count 0 is a merged duplicate (k_dd_merge, wcg_sort.h): no line
+// a record with count 0 is a merged duplicate (k_ss_bucket, wcg_sort.h: dd_same): no line
 __device__ __forceinline__ u64 line_len(const Rec& x, int fmt, u32 nreduce, u32 part, const uint8_t* arena) {
     if (x.cnt == 0 && fmt != FMT_COPY) return 0;
     if (fmt == FMT_MERGED) return rec_len(x) + 3 + ndigits(x.cnt);

@@ -329,6 +329,8 @@ struct SortArgs {
     Rec* irec;               // records by bucket (n) ...
     Rec* irec2;              // ... and the scratch of the oversized-bucket path (n)
     Rec* out;                // sorted records
+    u32 dedupe;              // merge repeated inline keys (record log jobs) while writing out
+    u64* nkeys;              // distinct keys (dedupe)
 };
 
 // sample j = record floor(j * n / S): stored in index order, so a stable sort gives the
@@ -408,7 +410,11 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) 
     ss_range(a, i0, i1);
     for (u64 i = i0 + threadIdx.x; i < i1; i += NT) {
         const Rec r = a.rec[i];
-        const u32 b = ss_find<SMALL>(a, r.hi, r.lo, (u32)i, sp_hi, sp_lo, sp_i);
+        // an inline key searches as (key, 0): every copy of a repeated key (record log jobs)
+        // lands in one bucket, so the bucket sort can merge them; long keys keep their index so
+        // equal 16-byte prefixes still spread over buckets
+        const u32 si = (r.ref & LONG_FLAG) ? (u32)i : 0u;
+        const u32 b = ss_find<SMALL>(a, r.hi, r.lo, si, sp_hi, sp_lo, sp_i);
         a.bid[i] = b;
         atomicAdd(&h[b], 1u);
     }
@@ -455,6 +461,28 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_scatter(SortArgs 
     for (u64 i = i0 + threadIdx.x; i < i1; i += NT) {
         const u32 d = atomicAdd(&cur[a.bid[i]], 1u);
         a.irec[d] = a.rec[i];
+    }
+}
+
+// Repeated inline keys (the record log of k_agg's pass 2 and the compacted tables may hold one
+// key more than once: the global table, other map calls, pass 2's overflow) are merged while a
+// bucket is written out: the first record of a run takes the run's total and the others count 0,
+// which formats to no line (wcg_reduce.h: line_len).  An inline key's 16-byte prefix is the whole
+// key (byte 15 is 0; a long key's is a letter byte), and long keys are never repeated.
+__device__ __forceinline__ bool dd_same(u64 ah, u64 al, u64 bh, u64 bl) {
+    return ah == bh && al == bl && (al & 0xFFu) == 0;
+}
+// distinct keys: one atomic per workgroup
+__device__ __forceinline__ void dd_count(const SortArgs& a, u32 heads) {
+    if (!a.dedupe) return;
+    __shared__ u32 wh[SB_NT / 64];
+    for (int d = 32; d >= 1; d >>= 1) heads += __shfl_xor(heads, d, 64);
+    if ((threadIdx.x & 63) == 0) wh[threadIdx.x >> 6] = heads;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u32 t = 0;
+        for (int w = 0; w < SB_NT / 64; w++) t += wh[w];
+        if (t) atomicAdd((unsigned long long*)a.nkeys, (unsigned long long)t);
     }
 }
 
@@ -514,7 +542,19 @@ __device__ void ss_global_sort(const SortArgs& a, u64 s, u64 m, u64* kh, u64* kl
         __syncthreads();
         const Rec* t = src; src = dst; dst = const_cast<Rec*>(t);
     }
-    for (u64 j = tid; j < m; j += SB_NT) a.out[s + j] = src[j];
+    u32 heads = 0;
+    for (u64 j = tid; j < m; j += SB_NT) {
+        Rec r = src[j];
+        if (a.dedupe) {
+            if (j > 0 && dd_same(src[j - 1].hi, src[j - 1].lo, r.hi, r.lo)) r.cnt = 0;
+            else {
+                heads++;
+                for (u64 q = j + 1; q < m && dd_same(r.hi, r.lo, src[q].hi, src[q].lo); q++) r.cnt += src[q].cnt;
+            }
+        }
+        a.out[s + j] = r;
+    }
+    dd_count(a, heads);
 }
 
 // one workgroup per bucket: bitonic sort of (hi, lo, position) in LDS, then the records are
@@ -535,35 +575,19 @@ __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
     __syncthreads();
     lds_bitonic<SB_NT>(kh, kl, kp, P);
     __syncthreads();
-    for (u32 j = threadIdx.x; j < m; j += SB_NT) a.out[s + j] = X[kp[j]];
-}
-
-// ---------------------------------------------------------------- duplicate keys
-// The record log of k_agg's pass 2 and the compacted tables may hold one key more than once
-// (the global table, other map calls, two slots claimed for one key by racing lanes): after the
-// sort such records are adjacent.  Inline records only (long keys live in the long-key table
-// alone): equal (hi, lo, ref = length).  Merged in place: the first record of a run takes the
-// run's total and the others count 0, which formats to no line (wcg_reduce.h: line_len); the
-// number of distinct keys goes to *nkeys.
-__device__ __forceinline__ bool dd_head(const Rec* r, u64 i) {
-    if (i == 0) return true;
-    const Rec& x = r[i];
-    const Rec& y = r[i - 1];
-    return (x.ref & LONG_FLAG) || (y.ref & LONG_FLAG) || x.hi != y.hi || x.lo != y.lo || x.ref != y.ref;
-}
-__global__ void k_dd_merge(Rec* r, u64 n, u64* nkeys) {
-    u64 heads = 0;
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
-        if (!dd_head(r, i)) continue;
-        heads++;
-        u64 j = i + 1;
-        if (j >= n || dd_head(r, j)) continue;      // no duplicate (nearly always)
-        u64 sum = r[i].cnt;
-        for (; j < n && !dd_head(r, j); j++) { sum += r[j].cnt; r[j].cnt = 0; }
-        r[i].cnt = sum;
+    u32 heads = 0;
+    for (u32 j = threadIdx.x; j < m; j += SB_NT) {
+        Rec r = X[kp[j]];
+        if (a.dedupe) {                               // sorted keys in LDS; counts from X (rare)
+            if (j > 0 && dd_same(kh[j - 1], kl[j - 1], kh[j], kl[j])) r.cnt = 0;
+            else {
+                heads++;
+                for (u32 q = j + 1; q < m && dd_same(kh[j], kl[j], kh[q], kl[q]); q++) r.cnt += X[kp[q]].cnt;
+            }
+        }
+        a.out[s + j] = r;
     }
-    for (int d = 32; d >= 1; d >>= 1) heads += __shfl_xor(heads, d, 64);
-    if ((threadIdx.x & 63) == 0 && heads) atomicAdd((unsigned long long*)nkeys, (unsigned long long)heads);
+    dd_count(a, heads);
 }
 
 // ---------------------------------------------------------------- tie groups
