@@ -395,9 +395,18 @@ int format(wcg_ctx* c, const Rec* r, u64 n, const uint8_t* base, int fmt, u32 nr
     RC(ensure(c, dbuf, cap, bound + 64));
     const u64 nt = cdiv(n, FM_TILE);
     RC(ensure(c, &c->lens, &c->lens_cap, nt + 1));
-    k_fmt_sum<<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, fmt, nreduce, part, base, c->lens);
+    switch (fmt) {
+#define WCG_FMT_SUM(F) case F: k_fmt_sum<F><<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, nreduce, part, base, c->lens); break;
+        WCG_FMT_SUM(FMT_MERGED) WCG_FMT_SUM(FMT_JSON) WCG_FMT_SUM(FMT_JSON_ALL) WCG_FMT_SUM(FMT_COPY)
+#undef WCG_FMT_SUM
+        default: c->err = "format: unknown format"; return WCG_EINVAL;
+    }
     k_scan_u64<<<1, 1024, 0, c->stream>>>(c->lens, nt, c->d_scalar);
-    k_fmt_write<<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, fmt, nreduce, part, base, c->lens, *dbuf);
+    switch (fmt) {
+#define WCG_FMT_WRITE(F) case F: k_fmt_write<F><<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, nreduce, part, base, c->lens, *dbuf); break;
+        WCG_FMT_WRITE(FMT_MERGED) WCG_FMT_WRITE(FMT_JSON) WCG_FMT_WRITE(FMT_JSON_ALL) WCG_FMT_WRITE(FMT_COPY)
+#undef WCG_FMT_WRITE
+    }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

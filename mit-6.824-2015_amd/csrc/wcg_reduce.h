@@ -41,10 +41,9 @@ __device__ __forceinline__ bool slot_to_rec(const GEntry* gtab, u64 gslots, cons
     const GEntry e = ltab[i - gslots];
     if (e.k0 == 0) return false;
     const u64 off = e.k1 - 1, len = e.aux;
-    u64 hi = 0, lo = 0;
-    for (int k = 0; k < 8; k++) hi = (hi << 8) | arena[off + k];
-    for (int k = 8; k < 16; k++) lo = (lo << 8) | arena[off + k];
-    r.hi = hi; r.lo = lo; r.cnt = e.cnt;
+    // the key's first 16 bytes: one aligned 16-byte load (arena cells are 16-byte aligned)
+    const uint4 q = *reinterpret_cast<const uint4*>(arena + off);
+    r.hi = bswap64((u64)q.y << 32 | q.x); r.lo = bswap64((u64)q.w << 32 | q.z); r.cnt = e.cnt;
     r.ref = LONG_FLAG | (len << 40) | off;
     return true;
 }
@@ -166,42 +165,51 @@ __device__ __forceinline__ u64 block_excl_scan(u64 s, u64* ws, u64& all) {
     return pre + incl - s;
 }
 
-__global__ __launch_bounds__(FM_NT) void k_fmt_sum(const Rec* r, u64 n, int fmt, u32 nreduce, u32 part,
-                                                  const uint8_t* arena, u64* tsum) {
+// a thread's FM_IPT records, loaded unconditionally (a load inside a per-record branch was a
+// serial chain of memory latencies); records past n are returned with count 0 and are not used
+__device__ __forceinline__ void fmt_load(const Rec* r, u64 n, u64 i0, Rec* x) {
+#pragma unroll
+    for (int k = 0; k < FM_IPT; k++) x[k] = r[i0 + k < n ? i0 + k : n - 1];
+}
+
+template <int FMT>
+__global__ __launch_bounds__(FM_NT) void k_fmt_sum(const Rec* r, u64 n, u32 nreduce, u32 part, const uint8_t* arena,
+                                                  u64* tsum) {
     __shared__ u64 ws[FM_NT / 64];
     const u64 i0 = (u64)blockIdx.x * FM_TILE + (u64)threadIdx.x * FM_IPT;
+    Rec x[FM_IPT];
+    fmt_load(r, n, i0, x);
     u64 s = 0;
-    for (int k = 0; k < FM_IPT; k++)
-        if (i0 + k < n) s += line_len(r[i0 + k], fmt, nreduce, part, arena);
+#pragma unroll
+    for (int k = 0; k < FM_IPT; k++) s += i0 + k < n ? line_len(x[k], FMT, nreduce, part, arena) : 0;
     u64 all;
     (void)block_excl_scan(s, ws, all);
     if (threadIdx.x == 0) tsum[blockIdx.x] = all;
 }
 
-// the lines of records r[i0, i0 + FM_IPT) with lengths L[] at o (global memory or LDS)
-template <typename P>
-__device__ __forceinline__ void fmt_lines(const Rec* r, u64 i0, const u64* L, int fmt, const uint8_t* arena, P o) {
+// the lines of records x[0, FM_IPT) with lengths L[] at o (global memory or LDS)
+template <int FMT, typename P>
+__device__ __forceinline__ void fmt_lines(const Rec* x, const u64* L, const uint8_t* arena, P o) {
     for (int q = 0; q < FM_IPT; q++) {
         if (L[q] == 0) continue;
-        const Rec x = r[i0 + q];
-        if (fmt == FMT_COPY) {
-            const uint8_t* src = arena + (x.ref & LONG_OFF_MASK);
+        if (FMT == FMT_COPY) {
+            const uint8_t* src = arena + (x[q].ref & LONG_OFF_MASK);
             for (u64 k = 0; k < L[q]; k++) o[k] = src[k];
             o += L[q];
             continue;
         }
-        const bool json = fmt != FMT_MERGED;
-        const u64 len = rec_len(x);
+        const bool json = FMT != FMT_MERGED;
+        const u64 len = rec_len(x[q]);
         if (json) {
             const char* pre = "{\"Key\":\"";
             for (int k = 0; k < 8; k++) *o++ = pre[k];
         }
-        if (x.ref & LONG_FLAG) {
-            const uint8_t* src = arena + (x.ref & LONG_OFF_MASK);
+        if (x[q].ref & LONG_FLAG) {
+            const uint8_t* src = arena + (x[q].ref & LONG_OFF_MASK);
             for (u64 k = 0; k < len; k++) *o++ = src[k];
         } else {
             for (u64 k = 0; k < len; k++)
-                *o++ = (uint8_t)(k < 8 ? x.hi >> (56 - 8 * k) : x.lo >> (56 - 8 * (k - 8)));
+                *o++ = (uint8_t)(k < 8 ? x[q].hi >> (56 - 8 * k) : x[q].lo >> (56 - 8 * (k - 8)));
         }
         if (json) {
             const char* mid = "\",\"Value\":\"";
@@ -209,8 +217,8 @@ __device__ __forceinline__ void fmt_lines(const Rec* r, u64 i0, const u64* L, in
         } else {
             *o++ = ':'; *o++ = ' ';
         }
-        const u32 nd = ndigits(x.cnt);
-        put_digits(o, x.cnt, nd);
+        const u32 nd = ndigits(x[q].cnt);
+        put_digits(o, x[q].cnt, nd);
         o += nd;
         if (json) { *o++ = '"'; *o++ = '}'; }
         *o++ = '\n';
@@ -221,14 +229,18 @@ __device__ __forceinline__ void fmt_lines(const Rec* r, u64 i0, const u64* L, in
 // 16-byte stores; the destination's alignment is kept by offsetting the LDS image by
 // (dst & 15).  A tile larger than the stage (long keys) writes its bytes directly.
 constexpr u32 FM_STAGE = 32768;
-__global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, int fmt, u32 nreduce, u32 part,
-                                                    const uint8_t* arena, const u64* toff, uint8_t* out) {
+template <int FMT>
+__global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, u32 nreduce, u32 part, const uint8_t* arena,
+                                                    const u64* toff, uint8_t* out) {
     __shared__ u64 ws[FM_NT / 64];
     __shared__ __align__(16) uint8_t sb[FM_STAGE];
     const u64 i0 = (u64)blockIdx.x * FM_TILE + (u64)threadIdx.x * FM_IPT;
+    Rec x[FM_IPT];
+    fmt_load(r, n, i0, x);
     u64 L[FM_IPT], s = 0;
+#pragma unroll
     for (int k = 0; k < FM_IPT; k++) {
-        L[k] = i0 + k < n ? line_len(r[i0 + k], fmt, nreduce, part, arena) : 0;
+        L[k] = i0 + k < n ? line_len(x[k], FMT, nreduce, part, arena) : 0;
         s += L[k];
     }
     u64 all;
@@ -236,10 +248,10 @@ __global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, int fm
     uint8_t* const dst = out + toff[blockIdx.x];
     const u32 pad = (u32)((uintptr_t)dst & 15);
     if (pad + all > FM_STAGE) {                     // workgroup-uniform
-        fmt_lines(r, i0, L, fmt, arena, dst + lo);
+        fmt_lines<FMT>(x, L, arena, dst + lo);
         return;
     }
-    fmt_lines(r, i0, L, fmt, arena, sb + pad + lo);
+    fmt_lines<FMT>(x, L, arena, sb + pad + lo);
     __syncthreads();
     uint8_t* const base = dst - pad;                // 16-byte aligned; sb[b] is base[b]
     const u32 total = pad + (u32)all;
