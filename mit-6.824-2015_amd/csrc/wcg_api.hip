@@ -40,6 +40,7 @@ struct wcg_ctx {
     DevState* st = nullptr;
     DevState* h_st = nullptr;                 // pinned mirror
     Rec* recA = nullptr; Rec* recB = nullptr; u64 rec_cap = 0;
+    Rec* crec = nullptr;                      // the compacted records: recA, or the record log
     Rec* sorted = nullptr;                    // recB, or a merge pass's last output
     u64* lens = nullptr; u64 lens_cap = 0;    // per-tile sums of the formatter
     u64* d_scalar = nullptr;                  // scan totals
@@ -215,8 +216,10 @@ int ensure_recs(wcg_ctx* c, u64 n) {
     return WCG_OK;
 }
 
-// tables -> recA; the record buffers start at max_keys records and grow (then the compaction
-// runs again) when the tables hold more keys than that
+// tables -> compacted records (c->crec).  Two-pass jobs append the tables' records to the
+// record log itself (no copy of the log); otherwise, or when the log's buffer cannot hold them,
+// the log is copied to the front of recA and the tables follow.  The record buffers start at
+// max_keys records and grow (then the compaction runs again) when the tables hold more keys.
 int compact(wcg_ctx* c) {
     if (c->compacted) return WCG_OK;
     // Two-pass jobs emit their inline keys as records; when nothing else reached the global
@@ -227,14 +230,32 @@ int compact(wcg_ctx* c) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         scan_gtab = c->h_st->global_ops != 0;
     }
+    const u64 gs = scan_gtab ? c->gslots : 0;
+    const u64 total = gs + c->lslots;
+    const u64 emit_cap = c->max_keys + 65536;     // the log's length: min(nemit, emit_cap)
+    if (c->two_pass_used && c->remit) {
+        HIPCHK(c, hipMemsetAsync(&c->st->nlong, 0, sizeof(u64), c->stream));
+        if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
+        k_log_len<<<1, 1, 0, c->stream>>>(emit_cap, c->st);
+        k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
+            c->gtab, gs, c->ltab, c->lslots, c->arena, c->remit, c->remit_cap, c->st);
+        HIPCHK(c, hipGetLastError());
+        if (c->timing) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
+        RC(check_status(c));
+        c->nrec = c->h_st->nrec;
+        if (c->nrec <= c->remit_cap) {
+            RC(ensure_recs(c, c->nrec));           // the sort's output
+            c->crec = c->remit;
+            c->compacted = true;
+            return WCG_OK;
+        }
+    }
     for (int pass = 0; pass < 2; pass++) {
         HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));   // nrec, nlong
         if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
         if (c->remit)                  // the record log of k_agg's pass 2 first (nrec = nemit)
             k_copy_emit<<<(unsigned)(c->ncu * 4), 256, 0, c->stream>>>(
-                c->remit, c->recA, std::min<u64>(c->rec_cap, c->max_keys + 65536), c->st);
-        const u64 gs = scan_gtab ? c->gslots : 0;
-        const u64 total = gs + c->lslots;
+                c->remit, c->recA, std::min<u64>(c->rec_cap, emit_cap), c->st);
         k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
             c->gtab, gs, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st);
         HIPCHK(c, hipGetLastError());
@@ -244,6 +265,7 @@ int compact(wcg_ctx* c) {
         if (c->nrec <= c->rec_cap) break;
         RC(ensure_recs(c, c->nrec));
     }
+    c->crec = c->recA;
     c->compacted = true;
     return WCG_OK;
 }
@@ -324,7 +346,7 @@ int sort_records(wcg_ctx* c) {
     c->sorted = c->recB;
     if (n == 0) return WCG_OK;
     if (n == 1) {
-        HIPCHK(c, hipMemcpyAsync(c->recB, c->recA, sizeof(Rec), hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->recB, c->crec, sizeof(Rec), hipMemcpyDeviceToDevice, c->stream));
         return WCG_OK;
     }
     if (n >= (1ull << 32)) { c->err = "sort: more than 2^32 distinct keys"; return WCG_EINVAL; }
@@ -334,7 +356,7 @@ int sort_records(wcg_ctx* c) {
     u64 target = target_env ? target_env : SS_TARGET;
     target = std::max<u64>(target, cdiv(n, SS_MAXB));
     SortArgs a;
-    a.rec = c->recA; a.n = n; a.out = c->recB;
+    a.rec = c->crec; a.n = n; a.out = c->recB;
     // the record log: a key may repeat (the global table, other map calls, pass 2's overflow):
     // the bucket sort merges the copies and counts the distinct keys
     a.dedupe = c->h_st->nemit != 0;
@@ -374,7 +396,7 @@ int sort_records(wcg_ctx* c) {
     k_ss_bucket<<<a.B, SB_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
     if (c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA));
-    c->compacted = false;          // recA was scratch for the ties
+    if (c->crec == c->recA) c->compacted = false;    // recA was scratch for the ties
     if (getenv("WCG_DEBUG"))
         fprintf(stderr, "wcg: nemit %llu global_ops %llu\n", (unsigned long long)c->h_st->nemit,
                 (unsigned long long)c->h_st->global_ops);
@@ -995,7 +1017,7 @@ int wcg_export_count(wcg_ctx* c, uint32_t nreduce, uint32_t nranks, uint64_t* co
     RC(ensure(c, &c->owner, &c->owner_cap, n + 1));
     HIPCHK(c, hipMemsetAsync(c->d_per_rank, 0, EX_MAX_RANKS * sizeof(u64), c->stream));
     if (n) {
-        k_export_count<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(c->recA, n, nreduce, nranks, c->arena,
+        k_export_count<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(c->crec, n, nreduce, nranks, c->arena,
                                                                             c->owner, c->d_per_rank);
         HIPCHK(c, hipGetLastError());
     }
@@ -1020,7 +1042,7 @@ int wcg_export_write(wcg_ctx* c, void* dev_dst) {
         HIPCHK(c, hipMemcpyAsync(c->d_per_rank + EX_MAX_RANKS, c->h_cur, c->exp_nranks * sizeof(u64),
                                  hipMemcpyHostToDevice, c->stream));
         k_export_write<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(
-            c->recA, n, c->exp_nranks, c->owner, c->d_per_rank + EX_MAX_RANKS, c->arena, (Rec*)dev_dst);
+            c->crec, n, c->exp_nranks, c->owner, c->d_per_rank + EX_MAX_RANKS, c->arena, (Rec*)dev_dst);
         HIPCHK(c, hipGetLastError());
     }
     c->exp_ready = false;          // the cursors were consumed (the pinned copy is in flight)

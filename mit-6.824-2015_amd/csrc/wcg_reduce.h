@@ -20,34 +20,8 @@ namespace wcg {
 // ---------------------------------------------------------------- compaction
 constexpr int CP_NT = 256, CP_IPT = 8;          // 2048 table slots per block, one atomic each
 
-__device__ __forceinline__ bool slot_to_rec(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 total, u64 i,
-                                            const uint8_t* arena, Rec& r) {
-    if (i < gslots) {
-        const GEntry e = gtab[i];
-        if (e.k0 == 0) return false;
-        if (key_short(e.k0)) {
-            r.hi = bswap64(e.k0 & 0x00FFFFFFFFFFFFFFull);
-            r.lo = 0;
-            r.ref = e.k0 >> 56;
-        } else {
-            r.hi = bswap64(e.k0);
-            r.lo = bswap64(e.k1 & 0x00FFFFFFFFFFFFFFull);
-            r.ref = e.k1 >> 56;
-        }
-        r.cnt = e.cnt;
-        return true;
-    }
-    if (i >= total) return false;
-    const GEntry e = ltab[i - gslots];
-    if (e.k0 == 0) return false;
-    const u64 off = e.k1 - 1, len = e.aux;
-    // the key's first 16 bytes: one aligned 16-byte load (arena cells are 16-byte aligned)
-    const uint4 q = *reinterpret_cast<const uint4*>(arena + off);
-    r.hi = bswap64((u64)q.y << 32 | q.x); r.lo = bswap64((u64)q.w << 32 | q.z); r.cnt = e.cnt;
-    r.ref = LONG_FLAG | (len << 40) | off;
-    return true;
-}
-
+// Each thread takes CP_IPT slots: every slot entry is loaded first, unconditionally (a load in a
+// per-slot branch made a serial chain of memory latencies), then long keys' 16-byte prefixes.
 __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
                                                   const uint8_t* arena, Rec* out, u64 cap, DevState* st) {
     __shared__ u32 wsum[CP_NT / 64];
@@ -55,14 +29,37 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
     const u64 total = gslots + lslots;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u64 b0 = (u64)blockIdx.x * CP_NT * CP_IPT;
+    GEntry e[CP_IPT];
+#pragma unroll
+    for (int j = 0; j < CP_IPT; j++) {
+        const u64 i = b0 + (u64)j * CP_NT + tid;
+        const GEntry* src = i < gslots ? gtab + i : ltab + (i < total ? i - gslots : lslots - 1);
+        e[j] = *src;
+        if (i >= total) e[j].k0 = 0;
+    }
+    uint4 q[CP_IPT];
+#pragma unroll
+    for (int j = 0; j < CP_IPT; j++) {
+        const bool lng = b0 + (u64)j * CP_NT + tid >= gslots && e[j].k0 != 0;
+        q[j] = *reinterpret_cast<const uint4*>(arena + (lng ? e[j].k1 - 1 : 0));   // arena cells: 16-byte aligned
+    }
     Rec r[CP_IPT];
     u32 have = 0, nlong = 0;
 #pragma unroll
-    for (int j = 0; j < CP_IPT; j++)
-        if (slot_to_rec(gtab, gslots, ltab, total, b0 + (u64)j * CP_NT + tid, arena, r[j])) {
-            have |= 1u << j;
-            nlong += (r[j].ref & LONG_FLAG) ? 1 : 0;
+    for (int j = 0; j < CP_IPT; j++) {
+        const GEntry& x = e[j];
+        if (x.k0 == 0) continue;
+        have |= 1u << j;
+        if (b0 + (u64)j * CP_NT + tid < gslots) {
+            r[j] = inline_rec(x.k0, x.k1, x.cnt);
+        } else {                                    // long key: {tag, arena offset + 1, cnt, len}
+            r[j].hi = bswap64((u64)q[j].y << 32 | q[j].x);
+            r[j].lo = bswap64((u64)q[j].w << 32 | q[j].z);
+            r[j].cnt = x.cnt;
+            r[j].ref = LONG_FLAG | (x.aux << 40) | (x.k1 - 1);
+            nlong++;
         }
+    }
     if (nlong) atomicAdd(&st->nlong, (u64)nlong);
     const u32 cnt = __popc(have);
     // block exclusive prefix of cnt (<= 8 per thread): 4 ballots per wave, then waves in order
@@ -85,6 +82,13 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
 #pragma unroll
     for (int j = 0; j < CP_IPT; j++)
         if (have & (1u << j)) { if (pos < cap) out[pos] = r[j]; pos++; }   // more: host grows, reruns
+}
+
+// two-pass jobs compact into the record log itself: the tables' records follow its
+// min(nemit, cap) records
+__global__ void k_log_len(u64 cap, DevState* st) {
+    const u64 n = st->nemit;
+    st->nrec = n < cap ? n : cap;
 }
 
 // the record log of k_agg's pass 2 -> the front of the compaction output (nrec = its length;
