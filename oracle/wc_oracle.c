@@ -252,3 +252,132 @@ WCO_API void wco_free(wco_result *r) {
     if (!r) return;
     free(r->keys); free(r->lens); free(r->counts); free(r);
 }
+
+/* ---------------- exact check of a merged file against the input, for inputs too large for
+ * wco_count (its per-thread tables, their merge and the final qsort take ~75 s per GiB of C4
+ * text).  The merged file is parsed into a table of its lines (format "key: count\n" with a
+ * decimal count > 0 and no leading zero, keys strictly ascending bytewise: Merge's sort.Strings
+ * + "%s: %s\n", mapreduce.go:284-321), then the input is tokenized exactly as wco_count does
+ * (FieldsFunc + IsLetter, wc.go:17-30) and every token decrements its line's count.  The file is
+ * right iff every token finds its line and every count ends at 0: the same multiset of
+ * (key, count) as the reference's, in the reference's order.  Returns 0, or an error code with
+ * a message in msg. */
+typedef struct { const uint8_t *key; uint32_t len; uint32_t hash; int64_t cnt; } vent_t;
+typedef struct {
+    const uint8_t *s; uint64_t n;
+    vent_t *t; uint64_t mask;
+    uint64_t tokens, missing, first_missing;
+} vjob_t;
+
+static vent_t *vfind(vent_t *t, uint64_t mask, const uint8_t *k, uint32_t len, uint32_t h) {
+    for (uint64_t i = h & mask;; i = (i + 1) & mask) {
+        vent_t *e = &t[i];
+        if (!e->hash) return NULL;
+        if (e->hash == h && e->len == len && memcmp(e->key, k, len) == 0) return e;
+    }
+}
+
+static void vtoken(vjob_t *j, uint64_t start, uint32_t len) {
+    const uint8_t *k = j->s + start;
+    vent_t *e = vfind(j->t, j->mask, k, len, khash(k, len));
+    j->tokens++;
+    if (e) __atomic_fetch_sub(&e->cnt, 1, __ATOMIC_RELAXED);
+    else if (j->missing++ == 0) j->first_missing = start;
+}
+
+static void *verify_job(void *arg) {
+    vjob_t *j = (vjob_t *)arg;
+    const uint8_t *s = j->s; uint64_t n = j->n, i = 0; int64_t start = -1;
+    while (i < n) {
+        uint8_t b = s[i];
+        int w = 1, let;
+        if (b < 0x80) let = ((uint32_t)(b | 0x20) - 'a') < 26u;
+        else { uint32_t cp; w = decode_rune(s, n, i, &cp); let = letter_rune(cp); }
+        if (let) { if (start < 0) start = (int64_t)i; }
+        else if (start >= 0) { vtoken(j, (uint64_t)start, (uint32_t)(i - start)); start = -1; }
+        i += w;
+    }
+    if (start >= 0) vtoken(j, (uint64_t)start, (uint32_t)(n - start));
+    return NULL;
+}
+
+WCO_API int wco_verify_merged(const uint8_t *s, uint64_t n, const uint8_t *m, uint64_t mlen, int nthreads,
+                              uint64_t *ntokens, uint64_t *nkeys, char *msg, uint64_t msgcap) {
+    uint64_t lines = 0;
+    for (uint64_t i = 0; i < mlen; i++) lines += m[i] == '\n';
+    if (mlen && m[mlen - 1] != '\n') { snprintf(msg, msgcap, "merged file does not end in a newline"); return 1; }
+    uint64_t cap = 1024; while (cap < 2 * lines + 2) cap <<= 1;
+    vent_t *t = (vent_t *)calloc(cap, sizeof(vent_t));
+    if (!t) { snprintf(msg, msgcap, "out of memory"); return 9; }
+    const uint8_t *pk = NULL; uint32_t pl = 0;
+    int rc = 0;
+    for (uint64_t p = 0, ln = 0; p < mlen; ln++) {
+        const uint8_t *nl = (const uint8_t *)memchr(m + p, '\n', mlen - p);
+        const uint8_t *line = m + p; uint64_t L = (uint64_t)(nl - line);
+        const uint8_t *colon = (const uint8_t *)memchr(line, ':', L);
+        if (!colon || colon == line || (uint64_t)(colon - line) + 2 >= L || colon[1] != ' ') {
+            snprintf(msg, msgcap, "line %llu: not \"key: count\"", (unsigned long long)ln); rc = 2; break;
+        }
+        uint32_t klen = (uint32_t)(colon - line);
+        const uint8_t *d = colon + 2; uint64_t nd = L - klen - 2; int64_t c = 0;
+        if (nd == 0 || nd > 19 || d[0] == '0') { snprintf(msg, msgcap, "line %llu: bad count", (unsigned long long)ln); rc = 2; break; }
+        for (uint64_t q = 0; q < nd; q++) {
+            if (d[q] < '0' || d[q] > '9') { rc = 2; break; }
+            c = c * 10 + (d[q] - '0');
+        }
+        if (rc) { snprintf(msg, msgcap, "line %llu: bad count", (unsigned long long)ln); break; }
+        if (pk) {
+            uint32_t mm = pl < klen ? pl : klen;
+            int cmp = memcmp(pk, line, mm);
+            if (cmp > 0 || (cmp == 0 && pl >= klen)) {
+                snprintf(msg, msgcap, "line %llu: keys not strictly ascending", (unsigned long long)ln); rc = 3; break;
+            }
+        }
+        pk = line; pl = klen;
+        uint32_t h = khash(line, klen);
+        for (uint64_t i = h & (cap - 1);; i = (i + 1) & (cap - 1))
+            if (!t[i].hash) { t[i].key = line; t[i].len = klen; t[i].hash = h; t[i].cnt = c; break; }
+        p = (uint64_t)(nl - m) + 1;
+    }
+    if (!rc) {
+        if (nthreads < 1) nthreads = 1;
+        if (n < (1u << 20)) nthreads = 1;
+        vjob_t *jobs = (vjob_t *)calloc((size_t)nthreads, sizeof(vjob_t));
+        pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+        uint64_t pos = 0;
+        for (int k = 0; k < nthreads; k++) {           /* cuts as in wco_count */
+            uint64_t end = (k == nthreads - 1) ? n : (n / nthreads) * (uint64_t)(k + 1);
+            if (end < pos) end = pos;
+            while (end < n && end > pos) {
+                uint8_t b = s[end - 1];
+                if (b < 0x80 && !(((uint32_t)(b | 0x20) - 'a') < 26u)) break;
+                end++;
+            }
+            jobs[k].s = s + pos; jobs[k].n = end - pos; jobs[k].t = t; jobs[k].mask = cap - 1;
+            pos = end;
+        }
+        for (int k = 0; k < nthreads; k++) pthread_create(&th[k], NULL, verify_job, &jobs[k]);
+        for (int k = 0; k < nthreads; k++) pthread_join(th[k], NULL);
+        uint64_t tok = 0;
+        for (int k = 0; k < nthreads; k++) {
+            tok += jobs[k].tokens;
+            if (jobs[k].missing && !rc) {
+                snprintf(msg, msgcap, "%llu input tokens have no line (first at byte %llu)",
+                         (unsigned long long)jobs[k].missing,
+                         (unsigned long long)(jobs[k].first_missing + (uint64_t)(jobs[k].s - s)));
+                rc = 4;
+            }
+        }
+        if (ntokens) *ntokens = tok;
+        if (nkeys) *nkeys = lines;
+        for (uint64_t i = 0; !rc && i < cap; i++)
+            if (t[i].hash && t[i].cnt != 0) {
+                snprintf(msg, msgcap, "key %.*s: count off by %lld", (int)(t[i].len < 64 ? t[i].len : 64), t[i].key,
+                         (long long)t[i].cnt);
+                rc = 5;
+            }
+        free(jobs); free(th);
+    }
+    free(t);
+    return rc;
+}

@@ -49,6 +49,9 @@ def lib() -> ctypes.CDLL:
         L.mrp_run_parallel.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.mrp_do_reduce.restype = None
         L.mrp_do_reduce.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        L.wco_verify_merged.restype = ctypes.c_int
+        L.wco_verify_merged.argtypes = [P, U64, P, U64, ctypes.c_int, ctypes.POINTER(U64), ctypes.POINTER(U64),
+                                        ctypes.c_char_p, U64]
         _lib = L
     return _lib
 
@@ -87,6 +90,19 @@ class Result:
 
 def merged(data: bytes, nthreads: int = 8) -> bytes:
     return Result(data, nthreads).merged()
+
+
+def verify_merged(data_ptr: int, n: int, merged: bytes, nthreads: int = 16):
+    """Exact check of a merged file against n input bytes at host address data_ptr, without
+    building the oracle's sorted result (wco_verify_merged: every input token decrements its
+    line's count; all must end at 0, keys strictly ascending).  For inputs too large for
+    Result (C4 at 64 GiB).  Returns (ok, message, ntokens, nkeys)."""
+    msg = ctypes.create_string_buffer(512)
+    nt, nk = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    mbuf = ctypes.create_string_buffer(merged, len(merged)) if merged else ctypes.create_string_buffer(1)
+    rc = lib().wco_verify_merged(data_ptr, n, ctypes.addressof(mbuf), len(merged), nthreads,
+                                 ctypes.byref(nt), ctypes.byref(nk), msg, 512)
+    return rc == 0, msg.value.decode(errors="replace"), nt.value, nk.value
 
 
 def tokens(data: bytes):
