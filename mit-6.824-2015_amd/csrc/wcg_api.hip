@@ -52,6 +52,7 @@ struct wcg_ctx {
     // sort (wcg_sort.h)
     Rec* smp = nullptr; u64 smp_cap = 0;      // 2 x sample records (merge ping-pong)
     u32* bid = nullptr; u64 bid_cap = 0;
+    u64* spx = nullptr; u64 spx_cap = 0;    // sort splitters as arrays (large B)
     Rec* irec = nullptr; u64 irec_cap = 0;
     LEnt* lent = nullptr; u64 lent_cap = 0;   // long-key partitions: LQ x lpart_cap entries
     u64* spill = nullptr; u64 spill_cap = 0;  // k_agg pass-1 spill regions
@@ -387,6 +388,12 @@ int sort_records(wcg_ctx* c) {
     RC(ensure(c, &c->irec, &c->irec_cap, 2 * n));
     a.bid = c->bid; a.hist = c->hist;
     a.irec = c->irec; a.irec2 = c->irec + n;
+    a.sph = a.spl = nullptr; a.spi = nullptr;
+    if (!small) {                                  // the splitters as arrays (hi, lo, index)
+        RC(ensure(c, &c->spx, &c->spx_cap, (u64)3 * a.B));
+        a.sph = c->spx; a.spl = c->spx + a.B; a.spi = reinterpret_cast<u32*>(c->spx + 2 * a.B);
+        k_ss_split<<<cdiv(a.B, 256), 256, 0, c->stream>>>(a);
+    }
     if (small) k_ss_hist<true><<<a.G, SS_NT, 0, c->stream>>>(a);
     else k_ss_hist<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
@@ -643,7 +650,7 @@ int wcg_close(wcg_ctx* c) {
     }
     void* bufs[] = {c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens, c->d_scalar, c->d_out,
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
-                    c->llog, c->llog_len, c->smp, c->bid, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->ovf, c->hist, c->spart, c->ikey, c->iidx, c->groups,
+                    c->llog, c->llog_len, c->smp, c->bid, c->spx, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->ovf, c->hist, c->spart, c->ikey, c->iidx, c->groups,
                     c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_st) (void)hipHostFree(c->h_st);

@@ -255,11 +255,58 @@ __device__ __forceinline__ u32 input_word(const MapArgs& a, u64 p, u32 len, u64 
     return rem >= 4 ? v : v & ((1u << (8 * rem)) - 1);
 }
 
-// do the long keys at input offsets p and q (both len bytes) have the same bytes?
+// aligned input dword at byte offset off (a multiple of 4); bytes past the input read as 0
+__device__ __forceinline__ u32 input_dword(const MapArgs& a, u64 off) {
+    if (off + 4 <= a.n) return *reinterpret_cast<const u32*>(a.in + off);
+    u32 v = 0;
+    for (u32 b = 0; b < 4; b++) if (off + b < a.n) v |= (u32)a.in[off + b] << (8 * b);
+    return v;
+}
+
+// key words j0 .. j0+7 of the key at input offset p (len bytes; zeros past len), from 9 aligned
+// dword loads issued together: a word-at-a-time loop waits for each load in turn, and these
+// loads go to HBM (long tokens are scattered over the input)
+__device__ __forceinline__ void input_words8(const MapArgs& a, u64 p, u32 len, u32 j0, u32* v) {
+    const u64 base = p + 4 * (u64)j0, q = base & ~3ull;
+    const u32 sh = (u32)(base & 3);
+    u32 d[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) d[k] = 4 * (j0 + k) < len + 4 ? input_dword(a, q + 4 * k) : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const u32 at = 4 * (j0 + k);
+        const u32 w = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        v[k] = at >= len ? 0u : (len - at >= 4 ? w : w & ((1u << (8 * (len - at))) - 1));
+    }
+}
+
+// FNV-1a 64 of the long key at input offset p (len bytes)
+__device__ __forceinline__ u64 input_fnv64(const MapArgs& a, u64 p, u32 len) {
+    u64 h = 0xCBF29CE484222325ull;
+    for (u32 j0 = 0; 4 * j0 < len; j0 += 8) {
+        u32 v[8];
+        input_words8(a, p, len, j0, v);
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                if (4 * (j0 + k) + b < len) { h ^= (v[k] >> (8 * b)) & 0xFFu; h *= 0x100000001B3ull; }
+    }
+    return h;
+}
+
+// do the long keys at input offsets p and q (both len bytes) have the same bytes?  (32 bytes of
+// both per round trip)
 __device__ __forceinline__ bool input_same(const MapArgs& a, u64 p, u64 q, u32 len) {
     if (p == q) return true;
     u32 diff = 0;
-    for (u64 j = 0; 4 * j < len && diff == 0; j++) diff |= input_word(a, p, len, j) ^ input_word(a, q, len, j);
+    for (u32 j0 = 0; 4 * j0 < len && diff == 0; j0 += 8) {
+        u32 x[8], y[8];
+        input_words8(a, p, len, j0, x);
+        input_words8(a, q, len, j0, y);
+#pragma unroll
+        for (int k = 0; k < 8; k++) diff |= x[k] ^ y[k];
+    }
     return diff == 0;
 }
 
@@ -341,12 +388,7 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
             if (len <= 15) { count_inline_run(a, p, len); len = 0; }
             else if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); len = 0; }
         } else if (len != 0) {
-            h = 0xCBF29CE484222325ull;
-            for (u32 j = 0; 4 * j < len; j++) {
-                const u32 v = input_word(a, p, (u32)len, j);
-                const u32 nb = len - 4 * j < 4 ? (u32)len - 4 * j : 4;
-                for (u32 b = 0; b < nb; b++) { h ^= (v >> (8 * b)) & 0xFFu; h *= 0x100000001B3ull; }
-            }
+            h = input_fnv64(a, p, (u32)len);
         }
         if (len != 0) {
             const u64 tag = long_tag(h, len), rec = p | len << 40;
@@ -375,13 +417,7 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
         const u64 rr = crec[e];
         if (rr == 0 || ccnt[e] == 0) continue;
         const u64 len = rr >> 40, p = rr & LLOG_OFF_MASK;
-        u64 h = 0xCBF29CE484222325ull;
-        for (u32 j = 0; 4 * j < len; j++) {
-            const u32 v = input_word(a, p, (u32)len, j);
-            const u32 nb = len - 4 * j < 4 ? (u32)len - 4 * j : 4;
-            for (u32 b = 0; b < nb; b++) { h ^= (v >> (8 * b)) & 0xFFu; h *= 0x100000001B3ull; }
-        }
-        emit(h, rr, ccnt[e]);
+        emit(input_fnv64(a, p, (u32)len), rr, ccnt[e]);
     }
 }
 

@@ -316,6 +316,10 @@ constexpr int SSL_NT = 1024;           // hist / scatter workgroups above SS_LDS
 constexpr u32 SS_TOP = 1024;           // top-level splitters staged in LDS above SS_LDSB buckets
 constexpr u32 SB_CAP = 2048;           // bucket records sorted in LDS (18 B each: 36 KiB)
 constexpr int SB_NT = 256;             // bucket sort workgroups
+#ifndef WCG_SS_U
+#define WCG_SS_U 4
+#endif
+constexpr int SS_U = WCG_SS_U;         // records per thread in flight (hist / scatter)
 
 struct SortArgs {
     const Rec* rec;          // compacted records (index = position)
@@ -331,6 +335,8 @@ struct SortArgs {
     Rec* out;                // sorted records
     u32 dedupe;              // merge repeated inline keys (record log jobs) while writing out
     u64* nkeys;              // distinct keys (dedupe)
+    u64* sph; u64* spl; u32* spi;   // splitters 0..B-2 as arrays (hi, lo, record index): the
+                                    // searches' global reads stay within 20 B per splitter (L2)
 };
 
 // sample j = record floor(j * n / S): stored in index order, so a stable sort gives the
@@ -348,6 +354,15 @@ __global__ void k_ss_sample(SortArgs a, Rec* smp) {
 // splitter b (0 <= b < B - 1) = sample (b + 1) * S / B; bucket(x) = number of splitters <= x in
 // the (hi, lo, record index) order - a total order, so equal prefixes spread over buckets
 __device__ __forceinline__ const Rec& ss_splitter(const SortArgs& a, u32 b) { return a.smp[(u64)(b + 1) * a.S / a.B]; }
+
+// the splitters as arrays (large B): 32768 splitters are 640 KiB, L2-resident, where the
+// sample records they come from span 8 MiB (one 128-byte line per splitter)
+__global__ void k_ss_split(SortArgs a) {
+    const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b + 1 >= a.B) return;
+    const Rec& s = ss_splitter(a, b);
+    a.sph[b] = s.hi; a.spl[b] = s.lo; a.spi[b] = (u32)s.cnt;
+}
 
 __device__ __forceinline__ void ss_range(const SortArgs& a, u64& i0, u64& i1) {
     i0 = a.n * blockIdx.x / a.G;
@@ -384,8 +399,9 @@ __device__ __forceinline__ u32 ss_find(const SortArgs& a, u64 hi, u64 lo, u32 id
     h = tl < SS_TOP ? ss_top_index(a, tl) : a.B - 1;
     while (l < h) {
         const u32 mid = (l + h) >> 1;
-        const Rec& s = ss_splitter(a, mid);
-        if (!key3_lt(hi, lo, idx, s.hi, s.lo, (u32)s.cnt)) l = mid + 1; else h = mid;
+        const u64 sh = a.sph[mid];
+        const bool lt = hi != sh ? hi < sh : key3_lt(hi, lo, idx, sh, a.spl[mid], a.spi[mid]);
+        if (!lt) l = mid + 1; else h = mid;
     }
     return l;
 }
@@ -401,18 +417,74 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) 
     for (u32 t = threadIdx.x; t < NSP; t += NT) {
         const bool live = SMALL ? t + 1 < a.B : true;
         if (live) {
-            const Rec& s = ss_splitter(a, SMALL ? t : ss_top_index(a, t));
-            sp_hi[t] = s.hi; sp_lo[t] = s.lo; sp_i[t] = (u32)s.cnt;
+            if (SMALL) {
+                const Rec& s = ss_splitter(a, t);
+                sp_hi[t] = s.hi; sp_lo[t] = s.lo; sp_i[t] = (u32)s.cnt;
+            } else {
+                const u32 k = ss_top_index(a, t);
+                sp_hi[t] = a.sph[k]; sp_lo[t] = a.spl[k]; sp_i[t] = a.spi[k];
+            }
         }
     }
     __syncthreads();
     u64 i0, i1;
     ss_range(a, i0, i1);
+    // an inline key searches as (key, 0): every copy of a repeated key (record log jobs) lands in
+    // one bucket, so the bucket sort can merge them; long keys keep their index so equal 16-byte
+    // prefixes still spread over buckets
+    if (!SMALL) {
+        // SS_U records per thread at a time: their global search steps issue together (each
+        // search is a chain of dependent L2 reads)
+        for (u64 i = i0 + threadIdx.x; i < i1; i += (u64)NT * SS_U) {
+            u64 hi[SS_U], lo[SS_U];
+            u32 si[SS_U], l[SS_U], m[SS_U];
+#pragma unroll
+            for (int k = 0; k < SS_U; k++) {
+                const u64 j = i + (u64)k * NT;
+                const Rec r = j < i1 ? a.rec[j] : Rec{~0ull, ~0ull, 0, 0};
+                hi[k] = r.hi; lo[k] = r.lo;
+                si[k] = (r.ref & LONG_FLAG) ? (u32)j : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < SS_U; k++) {
+                u32 tl = 0, th = SS_TOP;              // top splitters <= x (LDS)
+                while (tl < th) {
+                    const u32 mid = (tl + th) >> 1;
+                    if (!key3_lt(hi[k], lo[k], si[k], sp_hi[mid], sp_lo[mid], sp_i[mid])) tl = mid + 1; else th = mid;
+                }
+                l[k] = tl > 0 ? ss_top_index(a, tl - 1) + 1 : 0;
+                m[k] = (tl < SS_TOP ? ss_top_index(a, tl) : a.B - 1) - l[k];
+            }
+            while (true) {                            // lower bounds in [l, l + m), interleaved
+                bool any = false;
+                u64 sh[SS_U];
+#pragma unroll
+                for (int k = 0; k < SS_U; k++) {
+                    sh[k] = m[k] ? a.sph[l[k] + m[k] / 2] : 0;
+                    any |= m[k] != 0;
+                }
+                if (!any) break;
+#pragma unroll
+                for (int k = 0; k < SS_U; k++) {
+                    if (!m[k]) continue;
+                    const u32 half = m[k] / 2, mid = l[k] + half;
+                    const bool lt = hi[k] != sh[k] ? hi[k] < sh[k]
+                                                   : key3_lt(hi[k], lo[k], si[k], sh[k], a.spl[mid], a.spi[mid]);
+                    if (!lt) { l[k] = mid + 1; m[k] -= half + 1; } else m[k] = half;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < SS_U; k++) {
+                const u64 j = i + (u64)k * NT;
+                if (j < i1) { a.bid[j] = l[k]; atomicAdd(&h[l[k]], 1u); }
+            }
+        }
+        __syncthreads();
+        for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + blockIdx.x] = h[b];
+        return;
+    }
     for (u64 i = i0 + threadIdx.x; i < i1; i += NT) {
         const Rec r = a.rec[i];
-        // an inline key searches as (key, 0): every copy of a repeated key (record log jobs)
-        // lands in one bucket, so the bucket sort can merge them; long keys keep their index so
-        // equal 16-byte prefixes still spread over buckets
         const u32 si = (r.ref & LONG_FLAG) ? (u32)i : 0u;
         const u32 b = ss_find<SMALL>(a, r.hi, r.lo, si, sp_hi, sp_lo, sp_i);
         a.bid[i] = b;
@@ -458,9 +530,21 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_scatter(SortArgs 
     __syncthreads();
     u64 i0, i1;
     ss_range(a, i0, i1);
-    for (u64 i = i0 + threadIdx.x; i < i1; i += NT) {
-        const u32 d = atomicAdd(&cur[a.bid[i]], 1u);
-        a.irec[d] = a.rec[i];
+    // SS_U records per thread at a time: their loads, cursor atomics and stores issue together
+    for (u64 i = i0 + threadIdx.x; i < i1; i += (u64)NT * SS_U) {
+        u32 b[SS_U], d[SS_U];
+        Rec r[SS_U];
+#pragma unroll
+        for (int k = 0; k < SS_U; k++) {
+            const u64 j = i + (u64)k * NT;
+            if (j < i1) { b[k] = a.bid[j]; r[k] = a.rec[j]; }
+        }
+#pragma unroll
+        for (int k = 0; k < SS_U; k++)
+            if (i + (u64)k * NT < i1) d[k] = atomicAdd(&cur[b[k]], 1u);
+#pragma unroll
+        for (int k = 0; k < SS_U; k++)
+            if (i + (u64)k * NT < i1) a.irec[d[k]] = r[k];
     }
 }
 

@@ -41,14 +41,19 @@ def test_every_unicode_scalar(built, layout):
 
 
 @pytest.fixture(scope="module")
-def c4_gib(built):
-    import torch
+def c4_gen(built):
     from wcg.corpus import Generator, CONFIGS
     cfg = CONFIGS["c4_utf8_zipf_64gib"]
+    print("c4: building the 5e7-word generator", flush=True)
+    return Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"])
+
+
+@pytest.fixture(scope="module")
+def c4_gib(c4_gen):
+    import torch
     n = 1 << 30
     host = torch.empty(n, dtype=torch.uint8).pin_memory()
-    print("c4: building the 5e7-word generator", flush=True)
-    Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"]).fill_ptr(host.data_ptr(), n)
+    c4_gen.fill_ptr(host.data_ptr(), n)
     print("c4: 1 GiB generated", flush=True)
     return host
 
@@ -75,6 +80,35 @@ def test_c4_gib_5e7_key_table_multi_call(c4_gib):
     assert nk == r.nkeys and nk > 20_000_000
     assert st["tokens"] == r.ntokens and st["overflow"] == 0
     ob.assert_same(got, r.merged())
+
+
+@pytest.mark.timeout(600)
+def test_c4_4gib_sixteen_calls_record_log_overflow(c4_gen):
+    """Many DoMap calls into one two-pass job: 16 calls of 256 MiB emit ~1.3e8 pass-2 records,
+    more than the record log holds (max_keys), so later calls fall back to global-table inserts
+    and the reduce merges log and table.  Checked exactly by the oracle's verifier (the 64 GiB
+    run of tools/c4_full.py uses the same check)."""
+    import numpy as np
+    import torch
+    import wcg
+    n, q = 4 << 30, 256 << 20
+    host = np.empty(n, dtype=np.uint8)
+    c4_gen.fill_ptr(host.ctypes.data, n)
+    dev = torch.from_numpy(host).to("cuda")
+    torch.cuda.synchronize()
+    with wcg.Engine(0, 0, 50_000_000) as e:
+        e.reset()
+        for k in range(n // q):
+            e.map_device(dev.data_ptr() + k * q, q)
+        nk, _ = e.reduce()
+        got = e.result()
+        st = e.stats()
+    del dev
+    assert st["emitted"] > 50_000_000 + 65536 and st["global_ops"] > 0 and st["overflow"] == 0
+    print(f"c4 4 GiB: {nk} keys, {st['emitted']} records emitted; verifying", flush=True)
+    ok, msg, ntok, nkeys = ob.verify_merged(host.ctypes.data, n, got, 16)
+    assert ok, msg
+    assert ntok == st["tokens"] and nkeys == nk
 
 
 @pytest.mark.timeout(600)
