@@ -33,6 +33,8 @@ struct wcg_ctx {
     int ncu = 256;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t long_stream = nullptr;                // k_long_* beside k_agg (independent work)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     u64 max_input = 0, max_keys = 0;
     GEntry* gtab = nullptr; u64 gslots = 0;
     GEntry* ltab = nullptr; u64 lslots = 0;
@@ -364,7 +366,10 @@ int sort_records(wcg_ctx* c) {
     a.nkeys = c->d_scalar + 8;                     // its own slot (the scans use d_scalar[0])
     if (a.dedupe) HIPCHK(c, hipMemsetAsync(a.nkeys, 0, sizeof(u64), c->stream));
     a.B = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, target), SS_MAXB));
-    a.S = a.B > 1 ? std::min<u64>(n, (u64)a.B * SS_OVS) : 0;
+    // large sorts sample twice as densely: bucket sizes vary as 1/sqrt(samples per bucket), and a
+    // bucket past 4 * SB_NT records takes the 8-entry register network (twice the work per record)
+    const u64 ovs = a.B > SS_LDSB ? 2 * SS_OVS : SS_OVS;
+    a.S = a.B > 1 ? std::min<u64>(n, (u64)a.B * ovs) : 0;
     a.smp = nullptr;
     if (a.B > 1) {
         RC(ensure(c, &c->smp, &c->smp_cap, 2 * a.S));
@@ -400,7 +405,8 @@ int sort_records(wcg_ctx* c) {
     RC(scan_u32(c, c->hist, (u64)a.B * a.G));
     if (small) k_ss_scatter<true><<<a.G, SS_NT, 0, c->stream>>>(a);
     else k_ss_scatter<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
-    k_ss_bucket<<<a.B, SB_NT, 0, c->stream>>>(a);
+    k_ss_bucket<false><<<a.B, SB_NT, 0, c->stream>>>(a);
+    k_ss_bucket<true><<<a.B, SB_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
     if (c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA));
     if (c->crec == c->recA) c->compacted = false;    // recA was scratch for the ties
@@ -616,6 +622,9 @@ int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx** 
     *out = c;
     HIPCHK(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
     c->stream = c->own_stream;
+    HIPCHK(c, hipStreamCreateWithFlags(&c->long_stream, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     c->gslots = next_pow2(2 * c->max_keys);
     c->lslots = std::max<u64>(next_pow2(c->gslots / 4), 4096);
     c->arena_cap = std::max<u64>(64ull << 20, c->lslots * 32);   // heap part (after the slot cells)
@@ -640,7 +649,10 @@ int wcg_close(wcg_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    if (c->long_stream) (void)hipStreamSynchronize(c->long_stream);
     c->readers.reset();
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; i++) {
         if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
@@ -659,6 +671,7 @@ int wcg_close(wcg_ctx* c) {
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->long_stream) (void)hipStreamDestroy(c->long_stream);
     delete c;
     return WCG_OK;
 }
@@ -813,17 +826,25 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // workgroup's region), then one workgroup per partition.  Partition capacity: the log's
     // capacity spread evenly, with slack (the LDS cache folds hot keys before they are emitted;
     // a full partition falls back to exact per-entry inserts)
-    if (ablate == 0 || ablate >= 6) {
+    // They run on long_stream, forked after k_map and joined before this call returns: they and
+    // k_agg read k_map's outputs only and share nothing but atomic counters (the record log's
+    // cursor, the global table's claim protocol), and both are latency-bound (C4 1 GiB: 1.7 ms of
+    // long-key work beside 3.2 ms of aggregation)
+    const bool long_path = ablate == 0 || ablate >= 6;
+    if (long_path) {
+        HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->long_stream, c->ev_fork, 0));
         LongPart lp;
         const u64 expect = grid * (u64)a.tiles_per_wg * 16;     // 16 per step: 3x C4's rate
         lp.cap = (u32)std::min<u64>(std::max<u64>(1024, (expect * 5 / 4 + LQ - 1) / LQ), 0x7FFFFFFFull);
         RC(ensure(c, &c->lent, &c->lent_cap, (u64)LQ * lp.cap));
         RC(ensure(c, &c->lpcur, &c->lpcur_cap, (u64)LQ));
-        HIPCHK(c, hipMemsetAsync(c->lpcur, 0, LQ * sizeof(u32), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->lpcur, 0, LQ * sizeof(u32), c->long_stream));
         lp.ent = c->lent; lp.cur = c->lpcur;
-        k_long_hash<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, c->stream>>>(a, lp, (u32)grid);
-        k_long_agg<<<LQ, LONG_NT, 0, c->stream>>>(a, lp);
+        k_long_hash<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, c->long_stream>>>(a, lp, (u32)grid);
+        k_long_agg<<<LQ, LONG_NT, 0, c->long_stream>>>(a, lp);
         HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->ev_join, c->long_stream));
     }
     // k_agg pass 1 (spills what its LDS tables cannot hold) -> k_rp -> pass 2 (wcg_agg.h)
     AggArgs g;
@@ -864,6 +885,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     k_agg<<<grid2, AGG_NT, 0, c->stream>>>(g2);
     HIPCHK(c, hipGetLastError());
     }
+    if (long_path) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     if (c->timing) {
         e2 = take_event(c);
         HIPCHK(c, hipEventRecord(e2, c->stream));

@@ -24,7 +24,7 @@ constexpr int CP_NT = 256, CP_IPT = 8;          // 2048 table slots per block, o
 // per-slot branch made a serial chain of memory latencies), then long keys' 16-byte prefixes.
 __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
                                                   const uint8_t* arena, Rec* out, u64 cap, DevState* st) {
-    __shared__ u32 wsum[CP_NT / 64];
+    __shared__ u32 wsum[CP_NT / 64], wlong[CP_NT / 64];
     __shared__ u64 base_s;
     const u64 total = gslots + lslots;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -60,22 +60,25 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
             nlong++;
         }
     }
-    if (nlong) atomicAdd(&st->nlong, (u64)nlong);
     const u32 cnt = __popc(have);
-    // block exclusive prefix of cnt (<= 8 per thread): 4 ballots per wave, then waves in order
-    u32 o = 0, wt = 0;
+    // block exclusive prefix of cnt (<= 8 per thread): 4 ballots per wave, then waves in order;
+    // the long keys are summed the same way (one atomic per block: a per-thread atomic on one
+    // DevState word serialised ~1M times on C4, most of the kernel's 0.5 ms)
+    u32 o = 0, wt = 0, wl = 0;
 #pragma unroll
     for (int b = 0; b < 4; b++) {
         const u64 bal = __ballot((cnt >> b) & 1);
         o += __builtin_amdgcn_mbcnt_hi((u32)(bal >> 32), __builtin_amdgcn_mbcnt_lo((u32)bal, 0u)) << b;
         wt += (u32)__popcll(bal) << b;
+        wl += (u32)__popcll(__ballot((nlong >> b) & 1)) << b;
     }
-    if (lane == 0) wsum[w] = wt;
+    if (lane == 0) { wsum[w] = wt; wlong[w] = wl; }
     __syncthreads();
     if (tid == 0) {
-        u32 all = 0;
-        for (int k = 0; k < CP_NT / 64; k++) { const u32 v = wsum[k]; wsum[k] = all; all += v; }
+        u32 all = 0, al = 0;
+        for (int k = 0; k < CP_NT / 64; k++) { const u32 v = wsum[k]; wsum[k] = all; all += v; al += wlong[k]; }
         base_s = all ? atomicAdd(&st->nrec, (u64)all) : 0;
+        if (al) atomicAdd(&st->nlong, (u64)al);
     }
     __syncthreads();
     u64 pos = base_s + wsum[w] + o;

@@ -641,24 +641,107 @@ __device__ void ss_global_sort(const SortArgs& a, u64 s, u64 m, u64* kh, u64* kl
     dd_count(a, heads);
 }
 
-// one workgroup per bucket: bitonic sort of (hi, lo, position) in LDS, then the records are
-// permuted from the bucket's region (L2-resident) into place
+// ---- the bucket's bitonic network in registers: thread t holds entries i = t * E + e (e < E) of
+//      P = SB_NT * E.  Stages with compare distance j < E are register compare-exchanges, j < 64 E
+//      lane exchanges within the wave (__shfl_xor by j / E), and only j >= 64 E (3 of 55 stages
+//      for P = 1024) go through LDS with a workgroup barrier.  (An LDS network reads and writes
+//      both entries of every pair at every stage: 18 LDS operations per thread and stage.)
+__device__ __forceinline__ u64 shfl_xor64(u64 v, int d) {
+    const u32 lo = (u32)__shfl_xor((int)(u32)v, d, 64), hi = (u32)__shfl_xor((int)(u32)(v >> 32), d, 64);
+    return (u64)hi << 32 | lo;
+}
+template <int E, int J>
+__device__ __forceinline__ void rb_local(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u32 k) {
+    const u32 t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        if (e & J) continue;
+        const int f = e | J;
+        const bool asc = (((u32)(t * E + e)) & k) == 0;
+        if (key3_lt(h[f], l[f], q[f], h[e], l[e], q[e]) == asc) {
+            const u64 th = h[e], tl = l[e]; const u32 tq = q[e];
+            h[e] = h[f]; l[e] = l[f]; q[e] = q[f];
+            h[f] = th; l[f] = tl; q[f] = tq;
+        }
+    }
+}
+template <int E>
+__device__ __forceinline__ void reg_bitonic(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
+    constexpr u32 P = SB_NT * E;
+    const u32 t = threadIdx.x;
+    for (u32 k = 2; k <= P; k <<= 1)
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+            if (j < (u32)E) {
+                if (j == 1) rb_local<E, 1>(h, l, q, k);
+                else if (E > 2 && j == 2) rb_local<E, (E > 2 ? 2 : 1)>(h, l, q, k);
+                else if (E > 4 && j == 4) rb_local<E, (E > 4 ? 4 : 1)>(h, l, q, k);
+                continue;
+            }
+            u64 bh[E], bl[E];
+            u32 bq[E];
+            if (j < 64u * E) {
+                const int d = (int)(j / E);
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    bh[e] = shfl_xor64(h[e], d); bl[e] = shfl_xor64(l[e], d);
+                    bq[e] = (u32)__shfl_xor((int)q[e], d, 64);
+                }
+            } else {
+                __syncthreads();                      // the previous stage's readers are done
+#pragma unroll
+                for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = h[e]; kl[i] = l[e]; kp[i] = (uint16_t)q[e]; }
+                __syncthreads();
+#pragma unroll
+                for (int e = 0; e < E; e++) { const u32 i = (t * E + e) ^ j; bh[e] = kh[i]; bl[e] = kl[i]; bq[e] = kp[i]; }
+            }
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const u32 i = t * E + e;
+                const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+                if (key3_lt(bh[e], bl[e], bq[e], h[e], l[e], q[e]) == keep_min) { h[e] = bh[e]; l[e] = bl[e]; q[e] = bq[e]; }
+            }
+        }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = h[e]; kl[i] = l[e]; kp[i] = (uint16_t)q[e]; }
+    __syncthreads();
+}
+// load records X[0:m) as (hi, lo, position), padded to SB_NT * E entries, sort them, leave the
+// sorted entries in LDS
+template <int E>
+__device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* kl, uint16_t* kp) {
+    u64 h[E], l[E];
+    u32 q[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const u32 i = threadIdx.x * E + e;
+        if (i < m) { h[e] = X[i].hi; l[e] = X[i].lo; } else { h[e] = ~0ull; l[e] = ~0ull; }
+        q[e] = i;
+    }
+    reg_bitonic<E>(h, l, q, kh, kl, kp);
+}
+
+// one workgroup per bucket: bitonic sort of (hi, lo, position) in registers (LDS for the widest
+// stages), then the records are permuted from the bucket's region (L2-resident) into place
+// BIG = false: buckets of <= 4 * SB_NT records; true: the larger ones (their 8-entry networks
+// need more registers, which would cut the occupancy of every bucket if one kernel did both)
+template <bool BIG>
 __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
-    __shared__ u64 kh[SB_CAP], kl[SB_CAP];
-    __shared__ uint16_t kp[SB_CAP];
+    constexpr u32 CAP = BIG ? SB_CAP : 4 * SB_NT;  // 18 KiB of LDS for the small kernel: 6
+    __shared__ u64 kh[CAP], kl[CAP];               // workgroups per CU (the register limit)
+    __shared__ uint16_t kp[CAP];
     const u32 b = blockIdx.x;
     const u64 s = a.hist[(u64)b * a.G];
     const u64 e = b + 1 < a.B ? a.hist[(u64)(b + 1) * a.G] : a.n;
     const u64 m = e - s;
-    if (m == 0) return;
+    if (m == 0 || (m > 4 * SB_NT) != BIG) return;
     if (m > SB_CAP) { ss_global_sort(a, s, m, kh, kl, kp); return; }
-    u32 P = 64;
-    while (P < m) P <<= 1;
     const Rec* X = a.irec + s;
-    sb_load(X, (u32)m, P, kh, kl, kp);
-    __syncthreads();
-    lds_bitonic<SB_NT>(kh, kl, kp, P);
-    __syncthreads();
+    static_assert(SB_CAP == 8 * SB_NT, "k_ss_bucket's register networks cover SB_CAP entries");
+    if (BIG) sb_sort_regs<8>(X, (u32)m, kh, kl, kp);
+    else if (m <= SB_NT) sb_sort_regs<1>(X, (u32)m, kh, kl, kp);
+    else if (m <= 2 * SB_NT) sb_sort_regs<2>(X, (u32)m, kh, kl, kp);
+    else sb_sort_regs<4>(X, (u32)m, kh, kl, kp);
     u32 heads = 0;
     for (u32 j = threadIdx.x; j < m; j += SB_NT) {
         Rec r = X[kp[j]];
