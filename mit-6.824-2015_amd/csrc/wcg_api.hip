@@ -357,6 +357,9 @@ int sort_records(wcg_ctx* c) {
     const char* tenv = getenv("WCG_SORT_TARGET");
     const u64 target_env = tenv ? strtoull(tenv, nullptr, 10) : 0;
     u64 target = target_env ? target_env : SS_TARGET;
+    // small sorts: buckets small enough for two workgroups per CU (C2: 1e5 keys -> 512 buckets
+    // of ~200, one-entry networks) rather than fewer buckets than CUs
+    if (!target_env) target = std::min<u64>(target, std::max<u64>(128, n / (2ull * c->ncu)));
     target = std::max<u64>(target, cdiv(n, SS_MAXB));
     SortArgs a;
     a.rec = c->crec; a.n = n; a.out = c->recB;
@@ -368,7 +371,10 @@ int sort_records(wcg_ctx* c) {
     a.B = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, target), SS_MAXB));
     // large sorts sample twice as densely: bucket sizes vary as 1/sqrt(samples per bucket), and a
     // bucket past 4 * SB_NT records takes the 8-entry register network (twice the work per record)
-    const u64 ovs = a.B > SS_LDSB ? 2 * SS_OVS : SS_OVS;
+    // bucket past 4 * SB_NT records takes the 8-entry register network (twice the work per record);
+    // small sorts keep the sample within one workgroup's sort (TS_TILE) when 4+ per bucket allow
+    u64 ovs = a.B > SS_LDSB ? 2 * SS_OVS : SS_OVS;
+    if (a.B <= SS_LDSB && a.B * ovs > TS_TILE && a.B * 4 <= TS_TILE) ovs = TS_TILE / a.B;
     a.S = a.B > 1 ? std::min<u64>(n, (u64)a.B * ovs) : 0;
     a.smp = nullptr;
     if (a.B > 1) {

@@ -58,6 +58,71 @@ __device__ __forceinline__ void lds_bitonic(u64* kh, u64* kl, uint16_t* kp, u32 
         }
 }
 
+// ---- bitonic network in registers: thread t of NT holds entries i = t * E + e (e < E) of
+//      P = NT * E.  Stages with compare distance j < E are register compare-exchanges, j < 64 E
+//      lane exchanges within the wave (__shfl_xor by j / E), and only j >= 64 E (3 of 55 stages
+//      for P = 1024) go through LDS with a workgroup barrier.  (An LDS network reads and writes
+//      both entries of every pair at every stage: 18 LDS operations per thread and stage.)
+__device__ __forceinline__ u64 shfl_xor64(u64 v, int d) {
+    const u32 lo = (u32)__shfl_xor((int)(u32)v, d, 64), hi = (u32)__shfl_xor((int)(u32)(v >> 32), d, 64);
+    return (u64)hi << 32 | lo;
+}
+template <int E, int J>
+__device__ __forceinline__ void rb_local(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u32 k) {   // j = J < E
+    const u32 t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        if (e & J) continue;
+        const int f = e | J;
+        const bool asc = (((u32)(t * E + e)) & k) == 0;
+        if (key3_lt(h[f], l[f], q[f], h[e], l[e], q[e]) == asc) {
+            const u64 th = h[e], tl = l[e]; const u32 tq = q[e];
+            h[e] = h[f]; l[e] = l[f]; q[e] = q[f];
+            h[f] = th; l[f] = tl; q[f] = tq;
+        }
+    }
+}
+template <int NT, int E>
+__device__ __forceinline__ void reg_bitonic(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
+    constexpr u32 P = NT * E;
+    const u32 t = threadIdx.x;
+    for (u32 k = 2; k <= P; k <<= 1)
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+            if (j < (u32)E) {
+                if (j == 1) rb_local<E, 1>(h, l, q, k);
+                else if (E > 2 && j == 2) rb_local<E, (E > 2 ? 2 : 1)>(h, l, q, k);
+                else if (E > 4 && j == 4) rb_local<E, (E > 4 ? 4 : 1)>(h, l, q, k);
+                continue;
+            }
+            u64 bh[E], bl[E];
+            u32 bq[E];
+            if (j < 64u * E) {
+                const int d = (int)(j / E);
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    bh[e] = shfl_xor64(h[e], d); bl[e] = shfl_xor64(l[e], d);
+                    bq[e] = (u32)__shfl_xor((int)q[e], d, 64);
+                }
+            } else {
+                __syncthreads();                      // the previous stage's readers are done
+#pragma unroll
+                for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = h[e]; kl[i] = l[e]; kp[i] = (uint16_t)q[e]; }
+                __syncthreads();
+#pragma unroll
+                for (int e = 0; e < E; e++) { const u32 i = (t * E + e) ^ j; bh[e] = kh[i]; bl[e] = kl[i]; bq[e] = kp[i]; }
+            }
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const u32 i = t * E + e;
+                const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+                if (key3_lt(bh[e], bl[e], bq[e], h[e], l[e], q[e]) == keep_min) { h[e] = bh[e]; l[e] = bl[e]; q[e] = bq[e]; }
+            }
+        }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = h[e]; kl[i] = l[e]; kp[i] = (uint16_t)q[e]; }
+    __syncthreads();
+}
 // ---------------------------------------------------------------- merge sort (the sample, runs)
 // k_tile_sort orders each 2048-record tile by an LDS bitonic network, stable (ties by position),
 // then k_merge passes double the run length (A first on equal prefixes: stable).  A stable sort
@@ -500,18 +565,17 @@ __global__ __launch_bounds__(TS_NT) void k_ss_sample_sort(SortArgs a, Rec* smp) 
     __shared__ u64 sh[TS_TILE], sl[TS_TILE];
     __shared__ uint16_t si[TS_TILE];
     const int tid = threadIdx.x;
-    u32 P = 2;
-    while (P < a.S) P <<= 1;
-    for (u32 j = tid; j < P; j += TS_NT) {
-        if (j < a.S) {
-            const Rec r = a.rec[j * a.n / a.S];
-            sh[j] = r.hi; sl[j] = r.lo;
-        } else { sh[j] = ~0ull; sl[j] = ~0ull; }
-        si[j] = (uint16_t)j;
+    static_assert(TS_TILE == 2 * TS_NT, "the sample's register network: 2 entries per thread");
+    u64 h[2], l[2];
+    u32 q[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {                 // the register network of k_ss_bucket
+        const u32 j = tid * 2 + e;
+        if (j < a.S) { const Rec& r = a.rec[j * a.n / a.S]; h[e] = r.hi; l[e] = r.lo; }
+        else { h[e] = ~0ull; l[e] = ~0ull; }
+        q[e] = j;
     }
-    __syncthreads();
-    lds_bitonic<TS_NT>(sh, sl, si, P);
-    __syncthreads();
+    reg_bitonic<TS_NT, 2>(h, l, q, sh, sl, si);
     for (u32 j = tid; j < a.S; j += TS_NT) {
         Rec s;
         s.hi = sh[j]; s.lo = sl[j]; s.cnt = (u64)si[j] * a.n / a.S; s.ref = 0;
@@ -641,71 +705,6 @@ __device__ void ss_global_sort(const SortArgs& a, u64 s, u64 m, u64* kh, u64* kl
     dd_count(a, heads);
 }
 
-// ---- the bucket's bitonic network in registers: thread t holds entries i = t * E + e (e < E) of
-//      P = SB_NT * E.  Stages with compare distance j < E are register compare-exchanges, j < 64 E
-//      lane exchanges within the wave (__shfl_xor by j / E), and only j >= 64 E (3 of 55 stages
-//      for P = 1024) go through LDS with a workgroup barrier.  (An LDS network reads and writes
-//      both entries of every pair at every stage: 18 LDS operations per thread and stage.)
-__device__ __forceinline__ u64 shfl_xor64(u64 v, int d) {
-    const u32 lo = (u32)__shfl_xor((int)(u32)v, d, 64), hi = (u32)__shfl_xor((int)(u32)(v >> 32), d, 64);
-    return (u64)hi << 32 | lo;
-}
-template <int E, int J>
-__device__ __forceinline__ void rb_local(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u32 k) {
-    const u32 t = threadIdx.x;
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-        if (e & J) continue;
-        const int f = e | J;
-        const bool asc = (((u32)(t * E + e)) & k) == 0;
-        if (key3_lt(h[f], l[f], q[f], h[e], l[e], q[e]) == asc) {
-            const u64 th = h[e], tl = l[e]; const u32 tq = q[e];
-            h[e] = h[f]; l[e] = l[f]; q[e] = q[f];
-            h[f] = th; l[f] = tl; q[f] = tq;
-        }
-    }
-}
-template <int E>
-__device__ __forceinline__ void reg_bitonic(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
-    constexpr u32 P = SB_NT * E;
-    const u32 t = threadIdx.x;
-    for (u32 k = 2; k <= P; k <<= 1)
-        for (u32 j = k >> 1; j > 0; j >>= 1) {
-            if (j < (u32)E) {
-                if (j == 1) rb_local<E, 1>(h, l, q, k);
-                else if (E > 2 && j == 2) rb_local<E, (E > 2 ? 2 : 1)>(h, l, q, k);
-                else if (E > 4 && j == 4) rb_local<E, (E > 4 ? 4 : 1)>(h, l, q, k);
-                continue;
-            }
-            u64 bh[E], bl[E];
-            u32 bq[E];
-            if (j < 64u * E) {
-                const int d = (int)(j / E);
-#pragma unroll
-                for (int e = 0; e < E; e++) {
-                    bh[e] = shfl_xor64(h[e], d); bl[e] = shfl_xor64(l[e], d);
-                    bq[e] = (u32)__shfl_xor((int)q[e], d, 64);
-                }
-            } else {
-                __syncthreads();                      // the previous stage's readers are done
-#pragma unroll
-                for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = h[e]; kl[i] = l[e]; kp[i] = (uint16_t)q[e]; }
-                __syncthreads();
-#pragma unroll
-                for (int e = 0; e < E; e++) { const u32 i = (t * E + e) ^ j; bh[e] = kh[i]; bl[e] = kl[i]; bq[e] = kp[i]; }
-            }
-#pragma unroll
-            for (int e = 0; e < E; e++) {
-                const u32 i = t * E + e;
-                const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
-                if (key3_lt(bh[e], bl[e], bq[e], h[e], l[e], q[e]) == keep_min) { h[e] = bh[e]; l[e] = bl[e]; q[e] = bq[e]; }
-            }
-        }
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = h[e]; kl[i] = l[e]; kp[i] = (uint16_t)q[e]; }
-    __syncthreads();
-}
 // load records X[0:m) as (hi, lo, position), padded to SB_NT * E entries, sort them, leave the
 // sorted entries in LDS
 template <int E>
@@ -718,7 +717,7 @@ __device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* 
         if (i < m) { h[e] = X[i].hi; l[e] = X[i].lo; } else { h[e] = ~0ull; l[e] = ~0ull; }
         q[e] = i;
     }
-    reg_bitonic<E>(h, l, q, kh, kl, kp);
+    reg_bitonic<SB_NT, E>(h, l, q, kh, kl, kp);
 }
 
 // one workgroup per bucket: bitonic sort of (hi, lo, position) in registers (LDS for the widest
