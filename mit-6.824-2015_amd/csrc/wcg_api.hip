@@ -359,7 +359,7 @@ int sort_records(wcg_ctx* c) {
     u64 target = target_env ? target_env : SS_TARGET;
     // small sorts: buckets small enough for two workgroups per CU (C2: 1e5 keys -> 512 buckets
     // of ~200, one-entry networks) rather than fewer buckets than CUs
-    if (!target_env) target = std::min<u64>(target, std::max<u64>(128, n / (2ull * c->ncu)));
+    if (!target_env) target = std::min<u64>(target, std::max<u64>(128, cdiv(n, 2ull * c->ncu)));
     target = std::max<u64>(target, cdiv(n, SS_MAXB));
     SortArgs a;
     a.rec = c->crec; a.n = n; a.out = c->recB;
