@@ -36,6 +36,10 @@ constexpr u32 AGG_MAX_SRC = 256;       // source regions per workgroup (+1 KiB L
 constexpr u32 AGG_Q = 128;             // pass-2 sub-buckets per bucket
 constexpr u32 AGG_OVF_CAP = 4096;      // pass 2: overflow records staged per workgroup (128 KiB)
 constexpr int AGG_SPILL = 0, AGG_EMIT = 1;
+#ifndef WCG_AGG_SETS1
+#define WCG_AGG_SETS1 2
+#endif
+constexpr int AGG_SETS1 = WCG_AGG_SETS1;   // pass 1: wave batches in flight (pass 2: 2)
 
 struct AggArgs {
     // sources: bucket b's regions are pool + ((wbase + k * wstep) * rstride + b % rmod) * region_cap
@@ -87,11 +91,14 @@ __device__ __forceinline__ void agg_decode(const u64 (&u)[6], u64 (&k0)[4], u64 
 }
 
 // One (bucket, slice) of k_agg: index bi = p + P * s.  Returns the global-table inserts made.
+// MODE is a template parameter: one kernel for both passes held the union of their registers
+// (128 VGPRs with a spill)
+template <int MODE>
 __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[AGG_W], u64 (*tcnt)[AGG_W], u32* rlen_s,
                        u32* bstart, u32& spos, u64 (*wsum)[4]) {
     const int tid = threadIdx.x;
     LdsTable<AGG_NB, u64, AGG_W> tab{tk0, tk1, tcnt};
-    const bool emit = a.mode == AGG_EMIT;
+    constexpr bool emit = MODE == AGG_EMIT;
     const u32 p = bi % a.P, s = bi / a.P;
     u32 k0_, k1_, wbase, wstep;
     if (!emit) {
@@ -204,24 +211,31 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
             if (v[j + 1] && !tab.finish(k0[j + 1], k1[j + 1], pb, c[j + 1])) overflow(k0[j + 1], k1[j + 1], c[j + 1], nu[j + 1]);
         }
     };
-    u32 ka = 0, ba = 0;
-    if (per_wave) { ka = wave; ba = (u32)-1; advance(ka, ba, WSTRIDE); }
-    else advance(ka, ba, wave);
-    u32 kb = ka, bb = ba;
-    advance(kb, bb, WSTRIDE);
-    v4u a0, a1, a2, b0, b1, b2;
-    load(ka, ba, a0, a1, a2);
-    load(kb, bb, b0, b1, b2);
-    while (ka < nk) {
-        process(ka, ba, a0, a1, a2);
-        ka = kb; ba = bb;
-        advance(ka, ba, WSTRIDE);
-        load(ka, ba, a0, a1, a2);
-        if (kb >= nk) break;
-        process(kb, bb, b0, b1, b2);
-        kb = ka; bb = ba;
-        advance(kb, bb, WSTRIDE);
-        load(kb, bb, b0, b1, b2);
+    // NS batches in flight per wave: set s holds the wave's batch P + s; after processing it, it
+    // takes batch P + NS (the set before it, advanced once)
+    constexpr int NS = emit ? 2 : AGG_SETS1;
+    u32 kq[NS], bq[NS];
+    v4u x0[NS], x1[NS], x2[NS];
+    kq[0] = 0; bq[0] = 0;
+    if (per_wave) { kq[0] = wave; bq[0] = (u32)-1; advance(kq[0], bq[0], WSTRIDE); }
+    else advance(kq[0], bq[0], wave);
+#pragma unroll
+    for (int q = 1; q < NS; q++) { kq[q] = kq[q - 1]; bq[q] = bq[q - 1]; advance(kq[q], bq[q], WSTRIDE); }
+#pragma unroll
+    for (int q = 0; q < NS; q++) load(kq[q], bq[q], x0[q], x1[q], x2[q]);
+    bool more = kq[0] < nk;
+    while (more) {
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            if (more) {
+                if (kq[q] >= nk) { more = false; continue; }
+                process(kq[q], bq[q], x0[q], x1[q], x2[q]);
+                const int pq = (q + NS - 1) % NS;
+                kq[q] = kq[pq]; bq[q] = bq[pq];
+                advance(kq[q], bq[q], WSTRIDE);
+                load(kq[q], bq[q], x0[q], x1[q], x2[q]);
+            }
+        }
     }
     __syncthreads();
     if (!emit) {
@@ -282,6 +296,7 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
 // pass 1: one workgroup per (bucket, slice); pass 2: a persistent grid over the sub-buckets (most
 // are empty on low-cardinality text, and an empty one costs a few LDS reads instead of a launch
 // of a 160 KiB workgroup)
+template <int MODE>
 __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     __shared__ __align__(16) u64 tk0[AGG_NB][AGG_W];
     __shared__ __align__(16) u64 tk1[AGG_NB][AGG_W];
@@ -294,11 +309,11 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     const u32 nb = a.P * a.slices;
     u64 my_global = 0;
     for (u32 bi = blockIdx.x; bi < nb; bi += gridDim.x)
-        my_global += agg_one(a, bi, tk0, tk1, tcnt, rlen_s, bstart, spos, wsum);
+        my_global += agg_one<MODE>(a, bi, tk0, tk1, tcnt, rlen_s, bstart, spos, wsum);
     // one atomic per workgroup (a per-wave atomic on one DevState line serialises)
     for (int d = 32; d >= 1; d >>= 1) my_global += __shfl_xor(my_global, d, 64);
     u64 ms = 0;
-    if (blockIdx.x == 0 && a.mode != AGG_EMIT)  // k_map's stats: tokens, lds hits, global ops, long
+    if (blockIdx.x == 0 && MODE != AGG_EMIT)    // k_map's stats: tokens, lds hits, global ops, long
         for (u32 w = tid >> 2; w < a.nsrc; w += AGG_NT / 4) ms += a.map_stats[(u64)w * 4 + (tid & 3)];
     for (int d = 32; d >= 4; d >>= 1) ms += __shfl_xor(ms, d, 64);
     if ((tid & 63) < 4) wsum[tid >> 6][tid & 3] = ms + ((tid & 63) == 2 ? my_global : 0);

@@ -869,7 +869,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g.spill = c->spill; g.spill_len = c->spill_len;
     g.emit = c->remit; g.emit_cap = rec_cap_emit;
     g.ovf = nullptr; g.ovf_cap = 0;
-    k_agg<<<nb1, AGG_NT, 0, c->stream>>>(g);
+    k_agg<AGG_SPILL><<<nb1, AGG_NT, 0, c->stream>>>(g);
     HIPCHK(c, hipGetLastError());
     if (two_pass) {
     c->two_pass_used = true;
@@ -888,7 +888,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g2.ovf_cap = AGG_OVF_CAP;
     RC(ensure(c, &c->ovf, &c->ovf_cap, (u64)grid2 * AGG_OVF_CAP));
     g2.ovf = c->ovf;
-    k_agg<<<grid2, AGG_NT, 0, c->stream>>>(g2);
+    k_agg<AGG_EMIT><<<grid2, AGG_NT, 0, c->stream>>>(g2);
     HIPCHK(c, hipGetLastError());
     }
     if (long_path) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
