@@ -124,7 +124,7 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
     __syncthreads();
     const u32 nbat = bstart[nk];
     if (nbat == 0) {                                  // nothing to read (pass 2 on low-cardinality
-        if (!emit && tid == 0) a.spill_len[bi] = 0;   // text: every sub-bucket empty): done before
+        if (!emit && tid == 0 && a.spill_len) a.spill_len[bi] = 0;   // text: every sub-bucket empty): done before
         return 0;                                     // the table's 162 KiB are initialised
     }
     tab.init(tid, AGG_NT);
@@ -251,7 +251,7 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
             ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
         }
         __syncthreads();
-        if (tid == 0) a.spill_len[bi] = spos < a.spill_cap ? spos : (u32)a.spill_cap;
+        if (tid == 0 && a.spill_len) a.spill_len[bi] = spos < a.spill_cap ? spos : (u32)a.spill_cap;
     } else {
         // pass 2: this sub-bucket's keys, one record each, placed by one atomic per workgroup;
         // positions past the log's end go to the global table instead (the log stays dense:
@@ -326,28 +326,54 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     }
 }
 
-// k_rp: pass-1 workgroup b's spill -> its AGG_Q sub-bucket regions (b, q) of pool2, q = 7 bits of
-// the key's 64-bit hash (the 32-bit LDS hash's low bits, a single multiply away from the key
-// bytes, left C4's UTF-8 keys unevenly spread: sub-buckets overflowed their LDS tables).
+// k_rp (two-pass jobs): workgroup b = (bucket p, slice s) reads the miss-log regions of bucket p
+// written by the map workgroups of slice s and splits their entries into its AGG_Q sub-bucket
+// regions (b, q) of pool2, q = 7 bits of the key's 64-bit hash (the 32-bit LDS hash's low bits,
+// a single multiply away from the key bytes, left C4's UTF-8 keys unevenly spread: sub-buckets
+// overflowed their LDS tables).  (Until r02 a pass-1 k_agg aggregated each bucket slice in LDS
+// first and k_rp split its spill: on C4 that pass cut 126M units to 90M for 1.5 ms, more than
+// the 0.6 ms the smaller input saved k_rp and pass 2.)
 // Rounds of AGG_BATCH units: every lane appends its entries, whole, to its sub-bucket's LDS buffer
 // (or, when that buffer is full, straight to the region); then the buffers are written out
 // together.  The regions belong to this workgroup alone, so their cursors live in LDS too.  A full
-// region falls back to global-table inserts (exact).
+// region falls back to global-table inserts (exact).  Workgroup 0 also adds k_map's per-workgroup
+// stats to DevState (pass 1 does that in one-pass jobs).
 constexpr u32 RP_QB = 96;              // LDS units per sub-bucket buffer (96 KiB in all)
-__global__ __launch_bounds__(AGG_NT) void k_rp(const u64* spill, u64 spill_cap, const u32* spill_len, u64* pool2,
-                                               u64 cap2, u32* region_len2, GEntry* gtab, u64 gmask, DevState* st) {
+struct RpArgs {
+    const u64* pool; const u32* region_len; u64 region_cap;   // the miss log (k_map)
+    u32 P, nsrc, slices;                                       // buckets, map workgroups, slices
+    const u64* map_stats;
+    u64* pool2; u64 cap2; u32* region_len2;                    // sub-bucket regions (pass 2's input)
+    GEntry* gtab; u64 gmask; DevState* st;
+};
+__global__ __launch_bounds__(AGG_NT) void k_rp(RpArgs a) {
     __shared__ u64 sbuf[AGG_Q][RP_QB];
     __shared__ u32 scnt[AGG_Q], sfill[AGG_Q], gpos[AGG_Q], gbase[AGG_Q];
     __shared__ u32 sdirect[AGG_Q];            // 1: this round's buffer goes out entry by entry
+    __shared__ u64 wsum[AGG_NT / 64][4];
     const u32 b = blockIdx.x, tid = threadIdx.x;
-    const u32 n = spill_len[b];
-    if (n == 0) {                              // nothing spilled (low-cardinality text)
-        for (u32 q = tid; q < AGG_Q; q += AGG_NT) region_len2[(u64)b * AGG_Q + q] = 0;
-        return;
+    const u32 p = b % a.P, sl = b / a.P;
+    const u32 k0_ = (u32)(((u64)a.nsrc * sl) / a.slices), k1_ = (u32)(((u64)a.nsrc * (sl + 1)) / a.slices);
+    u64* const pool2 = a.pool2;
+    const u64 cap2 = a.cap2;
+    GEntry* const gtab = a.gtab;
+    const u64 gmask = a.gmask;
+    DevState* const st = a.st;
+    if (b == 0) {                              // k_map's stats: tokens, lds hits, global ops, long
+        u64 ms = 0;
+        for (u32 w = tid >> 2; w < a.nsrc; w += AGG_NT / 4) ms += a.map_stats[(u64)w * 4 + (tid & 3)];
+        for (int d = 32; d >= 4; d >>= 1) ms += __shfl_xor(ms, d, 64);
+        if ((tid & 63) < 4) wsum[tid >> 6][tid & 3] = ms;
+        __syncthreads();
+        if (tid < 4) {
+            u64 t = 0;
+            for (int w = 0; w < AGG_NT / 64; w++) t += wsum[w][tid];
+            u64* dst4[4] = {&st->tokens, &st->lds_hits, &st->global_ops, &st->long_tokens};
+            if (t) atomicAdd(dst4[tid], t);
+        }
     }
     for (u32 q = tid; q < AGG_Q; q += AGG_NT) { scnt[q] = 0; sfill[q] = 0; gpos[q] = 0; }
     __syncthreads();
-    const u64* src = spill + (u64)b * spill_cap;
     u64* const dst = pool2 + (u64)b * AGG_Q * cap2;
     u64 my_global = 0;
     auto encode = [](u64 k0, u64 k1, u64 c, u64 (&e)[3]) {
@@ -364,6 +390,10 @@ __global__ __launch_bounds__(AGG_NT) void k_rp(const u64* spill, u64 spill_cap, 
         my_global++;
         ginsert(gtab, gmask, k0, k1, gslot(key_hash(k0, k1)), c, st);
     };
+    for (u32 k = k0_; k < k1_; k++) {
+    const u64 reg = (u64)k * a.P + p;
+    const u32 n = a.region_len[reg];
+    const u64* src = a.pool + reg * a.region_cap;
     for (u32 base = 0; base < n; base += AGG_BATCH) {
         const u32 i0 = base + 4 * tid;
         u64 u[6];
@@ -418,7 +448,8 @@ __global__ __launch_bounds__(AGG_NT) void k_rp(const u64* spill, u64 spill_cap, 
         for (u32 q = tid; q < AGG_Q; q += AGG_NT) { scnt[q] = 0; sfill[q] = 0; }
         __syncthreads();
     }
-    for (u32 q = tid; q < AGG_Q; q += AGG_NT) region_len2[(u64)b * AGG_Q + q] = gpos[q] < cap2 ? gpos[q] : (u32)cap2;
+    }
+    for (u32 q = tid; q < AGG_Q; q += AGG_NT) a.region_len2[(u64)b * AGG_Q + q] = gpos[q] < cap2 ? gpos[q] : (u32)cap2;
     for (int d = 32; d >= 1; d >>= 1) my_global += __shfl_xor(my_global, d, 64);
     if ((tid & 63) == 0 && my_global) atomicAdd(&st->global_ops, my_global);
 }

@@ -55,6 +55,7 @@ struct wcg_ctx {
     Rec* smp = nullptr; u64 smp_cap = 0;      // 2 x sample records (merge ping-pong)
     u32* bid = nullptr; u64 bid_cap = 0;
     u64* spx = nullptr; u64 spx_cap = 0;    // sort splitters as arrays (large B)
+    bool nkeys_on_device = false;            // the sort's distinct-key count is still in d_scalar[8]
     Rec* irec = nullptr; u64 irec_cap = 0;
     LEnt* lent = nullptr; u64 lent_cap = 0;   // long-key partitions: LQ x lpart_cap entries
     u64* spill = nullptr; u64 spill_cap = 0;  // k_agg pass-1 spill regions
@@ -420,11 +421,9 @@ int sort_records(wcg_ctx* c) {
         fprintf(stderr, "wcg: nemit %llu global_ops %llu\n", (unsigned long long)c->h_st->nemit,
                 (unsigned long long)c->h_st->global_ops);
     c->nkeys = n;
-    if (a.dedupe) {
-        HIPCHK(c, hipMemcpyAsync(c->h_scalar, a.nkeys, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        c->nkeys = *c->h_scalar;
-    }
+    // record-log jobs count their distinct keys on the device (d_scalar[8]); the count is read
+    // with the formatted size at the end of wcg_reduce (one host round trip fewer)
+    c->nkeys_on_device = a.dedupe;
     return WCG_OK;
 }
 
@@ -449,7 +448,8 @@ int format(wcg_ctx* c, const Rec* r, u64 n, const uint8_t* base, int fmt, u32 nr
 #undef WCG_FMT_WRITE
     }
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    // the size, and the sort's distinct-key count (d_scalar[8]) in the same copy
+    HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, 9 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *nbytes = *c->h_scalar;
     return WCG_OK;
@@ -862,24 +862,28 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g.gtab = c->gtab; g.gmask = c->gslots - 1; g.st = c->st;
     g.map_stats = c->wg_stats;
     const u32 nb1 = P * g.slices;
-    // a workgroup spills at most what it reads: its slice's regions
-    g.spill_cap = two_pass ? (u64)cdiv(grid, g.slices) * a.region_cap : 0;
-    RC(ensure(c, &c->spill, &c->spill_cap, std::max<u64>(nb1 * g.spill_cap, 1)));
-    RC(ensure(c, &c->spill_len, &c->spill_len_cap, (u64)nb1));
-    g.spill = c->spill; g.spill_len = c->spill_len;
+    g.spill_cap = 0;                      // one pass: a full LDS table inserts into the global table
+    g.spill = nullptr; g.spill_len = nullptr;
     g.emit = c->remit; g.emit_cap = rec_cap_emit;
     g.ovf = nullptr; g.ovf_cap = 0;
-    k_agg<AGG_SPILL><<<nb1, AGG_NT, 0, c->stream>>>(g);
-    HIPCHK(c, hipGetLastError());
-    if (two_pass) {
+    if (!two_pass) {
+        k_agg<AGG_SPILL><<<nb1, AGG_NT, 0, c->stream>>>(g);
+        HIPCHK(c, hipGetLastError());
+    } else {
     c->two_pass_used = true;
-    // sub-bucket regions: 1.5x an even share of a spill region, a full one falls back to exact
-    // global inserts
-    const u64 cap2 = ((g.spill_cap * 3 / 2) / AGG_Q + 1024) & ~1ull;
+    // k_rp splits each (bucket, slice) of the miss log into AGG_Q sub-buckets; a sub-bucket region
+    // holds 1.5x an even share of what its slice's regions can hold, a full one falls back to
+    // exact global inserts
+    const u64 slice_cap = (u64)cdiv(grid, g.slices) * a.region_cap;
+    const u64 cap2 = ((slice_cap * 3 / 2) / AGG_Q + 1024) & ~1ull;
     RC(ensure(c, &c->pool2, &c->pool2_cap, (u64)nb1 * AGG_Q * cap2 + AGG_SLACK_UNITS));
     RC(ensure(c, &c->rlen2, &c->rlen2_cap, (u64)nb1 * AGG_Q));
-    k_rp<<<nb1, AGG_NT, 0, c->stream>>>(c->spill, g.spill_cap, c->spill_len, c->pool2, cap2, c->rlen2, c->gtab,
-                                        c->gslots - 1, c->st);
+    RpArgs rp;
+    rp.pool = c->pool; rp.region_len = c->region_len; rp.region_cap = a.region_cap;
+    rp.P = P; rp.nsrc = (u32)grid; rp.slices = g.slices; rp.map_stats = c->wg_stats;
+    rp.pool2 = c->pool2; rp.cap2 = cap2; rp.region_len2 = c->rlen2;
+    rp.gtab = c->gtab; rp.gmask = c->gslots - 1; rp.st = c->st;
+    k_rp<<<nb1, AGG_NT, 0, c->stream>>>(rp);
     AggArgs g2 = g;
     g2.pool = c->pool2; g2.region_len = c->rlen2; g2.region_cap = cap2;
     g2.P = P * AGG_Q; g2.nsrc = g.slices; g2.slices = 1;
@@ -954,6 +958,11 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
         c->phase_ev[4] = take_event(c);
         HIPCHK(c, hipEventRecord(c->phase_ev[4], c->stream));
         c->phase_rec = true;
+    }
+    if (c->nkeys_on_device) {
+        if (c->nrec == 0) c->nkeys = 0;               // format returned early: nothing sorted
+        else c->nkeys = c->h_scalar[8];
+        c->nkeys_on_device = false;
     }
     c->reduced = true;
     c->part_R = 0;
