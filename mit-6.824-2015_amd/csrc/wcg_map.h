@@ -64,6 +64,9 @@ constexpr int MAP_SETS = WCG_MAP_SETS;       // steps in flight per wave (2 or 4
 #ifndef WCG_MASKED_RESERVE
 #define WCG_MASKED_RESERVE 0                 // 1: miss reservations by the missing lanes only
 #endif
+#ifndef WCG_EVICT
+#define WCG_EVICT 0                          // 1: one refresh of the LDS table part-way (evict_at)
+#endif
 #ifndef WCG_WAIT0
 #define WCG_WAIT0 0                          // diagnostics: 1 = wait for every older memory op
 #endif
@@ -89,6 +92,8 @@ struct MapArgs {
     u64* llog;     u32 llog_cap;    // long-token log: region wg = llog[wg * llog_cap ...]
     u32* llog_len;                 // records written per region
     Rec* emit;     u64 emit_cap;    // two-pass jobs: the record log (k_long_hash's inline runs)
+    u32 evict_at;                   // WCG_EVICT: after this many steps per wave, the LDS table
+    u32 evict_min;                  //   drops entries counted fewer than evict_min times (0: never)
 };
 constexpr u64 LLOG_OFF_MASK = (1ull << 40) - 1;   // record = input offset | len << 40 (len 0: walk)
 constexpr u32 LLOG_PER_STEP = 64;                 // long-token log records per step: a bound (a
@@ -867,6 +872,31 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         }
     }
     u32 h1 = 0, h2 = 0, h3 = 0;
+    // WCG_EVICT: one refresh of the table once every wave has run evict_at steps (the host picks
+    // evict_at below every wave's step count, so all 16 waves reach the barriers): entries counted
+    // fewer than evict_min times go to the miss log with their counts and free their slots (and
+    // the admission filter restarts), so keys that became frequent since can take them.  Exact:
+    // every occurrence stays counted once, in the table or in the log.
+    u32 kstep = 0;
+    auto evict = [&]() {
+        __syncthreads();
+        auto out = [&](u64 k0, u64 k1, u32 c) {
+            if (!log_push(a, cursor, miss_bucket(lds_hash(k0, k1), a.pmask), k0, k1, c)) {
+                my_global++;
+                ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
+            }
+        };
+        for (int i = tid; i < MAP_NS; i += MAP_NT) {
+            const u32 c = scnt[i];
+            if (sk0[i] != 0 && c < a.evict_min) { if (c) out(sk0[i], 0, c); sk0[i] = 0; scnt[i] = 0; }
+        }
+        for (int i = tid; i < MAP_NM; i += MAP_NT) {
+            const u32 c = mcnt[i];
+            if (mk0[i] != 0 && c < a.evict_min) { if (c) out(mk0[i], mk1[i], c); mk0[i] = 0; mk1[i] = 0; mcnt[i] = 0; }
+        }
+        if (WCG_ADMIT2) for (int i = tid; i < (int)(MapTable<MAP_NS, MAP_NM>::ADMIT_BITS / 32); i += MAP_NT) seen_w[i] = 0;
+        __syncthreads();
+    };
 #define WCG_MAP_STEP(S)                                                                         \
     {                                                                                           \
         if (st >= nsteps || is_tail(st)) break;                                                 \
@@ -879,6 +909,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         set_load_##S(r, om, m##S);                                                              \
         h3 = h2; h2 = h1; h1 = it_;                                                             \
         st += stride;                                                                           \
+        if (WCG_EVICT && ++kstep == a.evict_at) evict();                                        \
     }
     while (true) {
         WCG_MAP_STEP(A)
