@@ -110,6 +110,13 @@ WCG_API int wcg_result_copy_device(wcg_ctx *ctx, void *dev_dst);
 /* Wait for all device work queued on the context's stream. */
 WCG_API int wcg_sync(wcg_ctx *ctx);
 
+/* Release a library-owned device buffer before the context is closed: the formatted output of
+ * wcg_result_device() or the records of wcg_export() (output buffers are
+ * library-owned until wcg_free).  Waits for the context's stream first.  Afterwards the result
+ * calls report WCG_ESTATE until the next wcg_reduce(); a later call that needs the buffer
+ * allocates it again.  Any other pointer: WCG_EINVAL. */
+WCG_API int wcg_free(wcg_ctx *ctx, const void *dev_ptr);
+
 /* Bytes of mrtmp.<f>-res-<r> (DoReduce output, mapreduce.go:264-279) for partition r of
  * nreduce, in sorted key order, copied to host_out (cap bytes).  *nbytes gets the size;
  * host_out == NULL queries the size only.  Requires a prior wcg_reduce(). */

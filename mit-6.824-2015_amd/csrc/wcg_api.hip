@@ -986,6 +986,28 @@ int wcg_result_device(wcg_ctx* c, const void** dev_ptr, uint64_t* nbytes) {
     return WCG_OK;
 }
 
+int wcg_free(wcg_ctx* c, const void* dev_ptr) {
+    if (!c) return WCG_EINVAL;
+    if (!dev_ptr) return WCG_OK;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    if (dev_ptr == c->d_out) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(c->d_out));
+        c->d_out = nullptr; c->out_cap = 0; c->out_len = 0;
+        c->reduced = false;
+        return WCG_OK;
+    }
+    if (dev_ptr == c->exp_buf) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(c->exp_buf));
+        c->exp_buf = nullptr; c->exp_cap = 0;
+        return WCG_OK;
+    }
+    c->err = "wcg_free: not a buffer this context handed out";
+    return WCG_EINVAL;
+}
+
 int wcg_result_copy(wcg_ctx* c, uint8_t* host_out, uint64_t cap) {
     if (!c) return WCG_EINVAL;
     if (!c->reduced) { c->err = "wcg_result_copy before wcg_reduce"; return WCG_ESTATE; }

@@ -24,7 +24,7 @@ EXPORTED = [
     "wcg_map_device", "wcg_reduce", "wcg_result_device", "wcg_result_copy", "wcg_partition",
     "wcg_export", "wcg_import", "wcg_timings", "wcg_enable_timing", "wcg_stats", "wcg_ihash",
     "wcg_version", "wcg_map_file", "wcg_partition_all", "wcg_map_json", "wcg_export_count",
-    "wcg_export_write", "wcg_merge_runs", "wcg_result_copy_device", "wcg_sync",
+    "wcg_export_write", "wcg_merge_runs", "wcg_result_copy_device", "wcg_sync", "wcg_free",
 ]
 
 
@@ -72,6 +72,7 @@ def load() -> ctypes.CDLL:
         "wcg_merge_runs": (I, [P, P, PU64, U32, PU64, PU64]),
         "wcg_result_copy_device": (I, [P, P]),
         "wcg_sync": (I, [P]),
+        "wcg_free": (I, [P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -205,6 +206,10 @@ class Engine:
 
     def sync(self) -> None:
         self._chk(self._lib.wcg_sync(self._ctx))
+
+    def free(self, dev_ptr: int) -> None:
+        """wcg_free: release the device buffer of result_device() or export() early."""
+        self._chk(self._lib.wcg_free(self._ctx, dev_ptr))
 
     def result(self) -> bytes:
         _, nb = self.result_device()

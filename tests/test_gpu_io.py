@@ -161,3 +161,30 @@ def test_dense_long_tokens_fill_the_log(eng):
     ob.assert_same(eng.result(), ob.merged(data))
     st = eng.stats()
     assert st["overflow"] == 0 and st["long_tokens"] == len(toks)
+
+
+def test_free_releases_result_and_export_buffers(built):
+    """wcg_free: the formatted output and the export records are library-owned
+    until freed; after the free the result calls report WCG_ESTATE, the next job works as usual,
+    and a pointer the context did not hand out is rejected."""
+    import wcg
+    from tests import oracle_bridge as ob
+    data = b"the cat and the hat\nand the bat\n" * 50
+    with wcg.Engine(0, 0, 1 << 16) as e:
+        e.reset()
+        e.map_host(data)
+        e.reduce()
+        ptr, nb = e.result_device()
+        assert nb == len(ob.merged(data))
+        e.free(ptr)
+        with pytest.raises(wcg.WcgError):
+            e.result()
+        dev, counts = e.export(3, 2)
+        assert sum(counts) > 0
+        e.free(dev)
+        with pytest.raises(wcg.WcgError):
+            e.free(12345)
+        e.reset()
+        e.map_host(data)
+        e.reduce()
+        assert e.result() == ob.merged(data)
