@@ -380,8 +380,8 @@ int sort_records(wcg_ctx* c) {
     a.smp = nullptr;
     if (a.B > 1) {
         RC(ensure(c, &c->smp, &c->smp_cap, 2 * a.S));
-        if (a.S <= TS_TILE) {                      // one workgroup samples and sorts
-            k_ss_sample_sort<<<1, TS_NT, 0, c->stream>>>(a, c->smp);
+        if (a.S <= TS_TILE) {                      // ranked in S / 64 workgroups
+            k_ss_rank_sort<<<(unsigned)cdiv(a.S, RK_SPB), RK_NT, 0, c->stream>>>(a, c->smp);
             a.smp = c->smp;
         } else {
             k_ss_sample<<<(unsigned)cdiv(a.S, 256), 256, 0, c->stream>>>(a, c->smp);

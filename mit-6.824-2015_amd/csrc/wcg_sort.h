@@ -559,28 +559,31 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) 
     for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + blockIdx.x] = h[b];
 }
 
-// the sample of a small sort (S <= TS_TILE): gathered and sorted in one workgroup's LDS,
-// stable (ties by sample position = record order)
-__global__ __launch_bounds__(TS_NT) void k_ss_sample_sort(SortArgs a, Rec* smp) {
+// the sample of a small sort (S <= TS_TILE) by ranks: rank = the samples below it in the
+// (hi, lo, sample index) order, a permutation.  One wave per sample: its 64 lanes compare the
+// sample with S / 64 entries each of the sample staged in LDS, and the counts are summed across
+// the wave.  (A one-workgroup network over 2048 entries took 37 us - 66 stages of lane exchanges
+// on one CU; fewer lanes per sample left one long compare loop per wave, 49-195 us.)
+constexpr int RK_NT = 256, RK_SPB = RK_NT / 64;   // samples per block: one per wave
+__global__ __launch_bounds__(RK_NT) void k_ss_rank_sort(SortArgs a, Rec* smp) {
     __shared__ u64 sh[TS_TILE], sl[TS_TILE];
-    __shared__ uint16_t si[TS_TILE];
-    const int tid = threadIdx.x;
-    static_assert(TS_TILE == 2 * TS_NT, "the sample's register network: 2 entries per thread");
-    u64 h[2], l[2];
-    u32 q[2];
+    const u32 S = (u32)a.S;
+    for (u32 j = threadIdx.x; j < S; j += RK_NT) {
+        const Rec& r = a.rec[j * a.n / S];
+        sh[j] = r.hi; sl[j] = r.lo;
+    }
+    __syncthreads();
+    const u32 j = blockIdx.x * RK_SPB + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= S) return;                      // wave-uniform
+    const u64 h = sh[j], l = sl[j];
+    u32 rank = 0;
+    for (u32 k = lane; k < S; k += 64) rank += key3_lt(sh[k], sl[k], k, h, l, j) ? 1u : 0u;
 #pragma unroll
-    for (int e = 0; e < 2; e++) {                 // the register network of k_ss_bucket
-        const u32 j = tid * 2 + e;
-        if (j < a.S) { const Rec& r = a.rec[j * a.n / a.S]; h[e] = r.hi; l[e] = r.lo; }
-        else { h[e] = ~0ull; l[e] = ~0ull; }
-        q[e] = j;
-    }
-    reg_bitonic<TS_NT, 2>(h, l, q, sh, sl, si);
-    for (u32 j = tid; j < a.S; j += TS_NT) {
-        Rec s;
-        s.hi = sh[j]; s.lo = sl[j]; s.cnt = (u64)si[j] * a.n / a.S; s.ref = 0;
-        smp[j] = s;
-    }
+    for (int d = 32; d >= 1; d >>= 1) rank += __shfl_xor((int)rank, d, 64);
+    if (lane != 0) return;
+    Rec o;
+    o.hi = h; o.lo = l; o.cnt = (u64)j * a.n / S; o.ref = 0;
+    smp[rank] = o;
 }
 
 // records of workgroup g go to [hist[b][g], ...) of their bucket, whole (the bucket sort then
