@@ -189,32 +189,31 @@ def main():
     keys_cap = max(min(4 * cfg["vocab"], n // 32), 1 << 18)
     eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=keys_cap)
     eng.set_stream(stream)
-    eng.enable_timing(True)
+    # HIP events around every kernel phase of every job, summed by the engine and read once after
+    # the timed loop (timing mode 2: no per-step host read of the events)
+    eng.enable_timing(2)
     teng = wd.TorchEngine(eng, stream, host_staging=gloo)
 
     def step():
-        """one job; returns the device ms per phase of this rank's map (and, N = 1, reduce)"""
+        """one job: this rank's map (N = 1: + DoReduce and Merge; N > 1: + shuffle, owners'
+        DoReduce, Merge of the runs at rank 0)"""
         eng.reset()
         eng.map_device(dev.data_ptr(), n)
         if world == 1:
             eng.reduce()
-            return eng.timings()[0]
-        ph = eng.timings()[0]                 # taken before the shuffle's reset clears them
+            return
         wd.shuffle_reduce(teng, args.nreduce)            # owners: DoReduce of their partitions
         wd.gather_merge(teng, fetch=False)               # rank 0: k-way merge of the sorted runs
-        return ph
 
     for _ in range(args.warmup):
         step()
-    map_ms, phase_ms = [], []
+    eng.enable_timing(2)                      # a new epoch: the timed steps only
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ph = step()
-        map_ms.append(ph["map"])
-        phase_ms.append(ph)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -224,6 +223,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     stats = eng.stats() if world == 1 else None
+    ph_sum, map_launches = eng.timings()          # device ms per phase, summed over the timed steps
+    assert map_launches == args.steps, (map_launches, args.steps)
 
     # ---- verify the last step's output against the oracle (outside the timed region)
     verified = None
@@ -258,7 +259,7 @@ def main():
         ms_step = dt / args.steps * 1e3
         all_bytes = total if strong else n * world
         gbs = all_bytes / (dt / args.steps) / 1e9
-        avg_map_ms = sum(map_ms) / len(map_ms)
+        avg_map_ms = ph_sum["map"] / args.steps
         achieved = n / (avg_map_ms * 1e-3) / 1e9 if avg_map_ms > 0 else None
         traffic = None
         try:
@@ -297,7 +298,7 @@ def main():
         }
         if stats:
             out["stats"] = stats
-        out["phase_ms_avg"] = {k: round(sum(p[k] for p in phase_ms) / len(phase_ms), 4) for k in phase_ms[0]}
+        out["phase_ms_avg"] = {k: round(v / args.steps, 4) for k, v in ph_sum.items()}
         out["verified_vs_oracle"] = verified
         if world == 1 and not args.no_end_to_end:
             out["end_to_end"] = end_to_end(eng, cfg, n)

@@ -171,7 +171,9 @@ WCG_API int wcg_merge_runs(wcg_ctx *ctx, const void *dev_text, const uint64_t *r
  * (k_long_hash, k_long_agg, k_agg pass 1, k_rp, k_agg pass 2), ms[2] compaction,
  * ms[3] sort, ms[4] format.  n = number of doubles the caller provides (<= 5). */
 WCG_API int wcg_timings(wcg_ctx *ctx, double *ms, int n, uint64_t *map_launches);
-/* Enable/disable the event timing above (off by default: it adds event records). */
+/* Enable/disable the event timing above (off by default: it adds event records).  on = 1: the
+ * phases of the last job; on = 2: every job from this call on, summed (wcg_reset keeps the events,
+ * so a timed loop needs no wcg_timings call, and no host round trip, between its jobs). */
 WCG_API int wcg_enable_timing(wcg_ctx *ctx, int on);
 
 /* Diagnostics, stats9 = {tokens, distinct keys, tokens counted in LDS, global-table operations,

@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -116,6 +117,9 @@ struct wcg_ctx {
     size_t ev_used = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> map_ev, agg_ev;
     hipEvent_t phase_ev[6] = {};
+    u64 map_launches_since_reset = 0;
+    int timing_mode = 0;                     // 1: the last job; 2: every job since enable (no reads in between)
+    std::vector<std::array<hipEvent_t, 5>> phase_jobs;   // mode 2: each job's phase events
     bool phase_rec = false;
     u64 map_launches = 0;
     std::string err;
@@ -691,6 +695,11 @@ int wcg_set_stream(wcg_ctx* c, void* stream) {
 int wcg_enable_timing(wcg_ctx* c, int on) {
     if (!c) return WCG_EINVAL;
     c->timing = on != 0;
+    c->timing_mode = on == 2 ? 2 : (on ? 1 : 0);
+    if (c->timing_mode == 2) {           // a new accumulation epoch
+        c->map_ev.clear(); c->agg_ev.clear(); c->phase_jobs.clear();
+        c->ev_used = 0; c->map_launches = 0; c->phase_rec = false;
+    }
     return WCG_OK;
 }
 
@@ -701,12 +710,18 @@ int wcg_reset(wcg_ctx* c) {
     // The global table (up to GBs) is cleared only if something may have written it since it was
     // last cleared: every kernel that inserts into it counts global_ops, and wcg_import sets
     // `imported`; two-pass jobs normally leave it empty.
+    // One-pass map calls flush their tables into it, so only after two-pass calls is it worth a
+    // host round trip to ask; with no map call since the last clear it is still clear.
     bool clear_g = true;
     if (c->gtab_zero && !c->imported) {
-        HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        clear_g = c->h_st->global_ops != 0;
+        if (c->map_launches_since_reset == 0) clear_g = false;
+        else if (c->two_pass_used) {
+            HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            clear_g = c->h_st->global_ops != 0;
+        }
     }
+    c->map_launches_since_reset = 0;
     if (clear_g) HIPCHK(c, hipMemsetAsync(c->gtab, 0, c->gslots * sizeof(GEntry), c->stream));
     c->gtab_zero = true;
     HIPCHK(c, hipMemsetAsync(c->ltab, 0, c->lslots * sizeof(GEntry), c->stream));
@@ -716,11 +731,13 @@ int wcg_reset(wcg_ctx* c) {
     c->part_R = 0;
     c->nrec = 0;
     c->out_len = 0;
-    c->map_ev.clear();
-    c->agg_ev.clear();
-    c->ev_used = 0;
-    c->phase_rec = false;
-    c->map_launches = 0;
+    if (c->timing_mode != 2) {          // mode 2 keeps every job's events until wcg_timings
+        c->map_ev.clear();
+        c->agg_ev.clear();
+        c->ev_used = 0;
+        c->phase_rec = false;
+        c->map_launches = 0;
+    }
     c->two_pass_used = false;
     c->imported = false;
     return WCG_OK;
@@ -910,6 +927,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         c->agg_ev.push_back({e1, e2});
     }
     c->map_launches++;
+    c->map_launches_since_reset++;
     c->compacted = c->reduced = false;
     c->exp_ready = false;
     c->part_R = 0;
@@ -965,6 +983,8 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
         c->phase_ev[4] = take_event(c);
         HIPCHK(c, hipEventRecord(c->phase_ev[4], c->stream));
         c->phase_rec = true;
+        if (c->timing_mode == 2)
+            c->phase_jobs.push_back({c->phase_ev[0], c->phase_ev[1], c->phase_ev[2], c->phase_ev[3], c->phase_ev[4]});
     }
     if (c->nkeys_on_device) {
         if (c->nrec == 0) c->nkeys = 0;               // format returned early: nothing sorted
@@ -1264,7 +1284,13 @@ int wcg_timings(wcg_ctx* c, double* ms, int n, uint64_t* map_launches) {
     float f = 0;
     for (auto& p : c->map_ev) { HIPCHK(c, hipEventElapsedTime(&f, p.first, p.second)); v[0] += f; }
     for (auto& p : c->agg_ev) { HIPCHK(c, hipEventElapsedTime(&f, p.first, p.second)); v[1] += f; }
-    if (c->phase_rec) {
+    if (c->timing_mode == 2) {          // summed over every job of the epoch
+        for (auto& j : c->phase_jobs) {
+            HIPCHK(c, hipEventElapsedTime(&f, j[0], j[1])); v[2] += f;
+            HIPCHK(c, hipEventElapsedTime(&f, j[2], j[3])); v[3] += f;
+            HIPCHK(c, hipEventElapsedTime(&f, j[3], j[4])); v[4] += f;
+        }
+    } else if (c->phase_rec) {
         HIPCHK(c, hipEventElapsedTime(&f, c->phase_ev[0], c->phase_ev[1])); v[2] = f;
         HIPCHK(c, hipEventElapsedTime(&f, c->phase_ev[2], c->phase_ev[3])); v[3] = f;
         HIPCHK(c, hipEventElapsedTime(&f, c->phase_ev[3], c->phase_ev[4])); v[4] = f;

@@ -161,8 +161,11 @@ class Engine:
     def set_stream(self, stream_ptr: int) -> None:
         self._chk(self._lib.wcg_set_stream(self._ctx, ctypes.c_void_p(stream_ptr)))
 
-    def enable_timing(self, on: bool = True) -> None:
-        self._chk(self._lib.wcg_enable_timing(self._ctx, 1 if on else 0))
+    def enable_timing(self, on=True) -> None:
+        """on = True/1: phase times of the last job; 2: summed over every job from now on (no
+        timings() call, hence no host round trip, needed between jobs); False/0: off."""
+        mode = 2 if on == 2 and on is not True else (1 if on else 0)
+        self._chk(self._lib.wcg_enable_timing(self._ctx, mode))
 
     # -- phases
     def reset(self) -> None:
