@@ -261,7 +261,8 @@ int compact(wcg_ctx* c) {
     for (int pass = 0; pass < 2; pass++) {
         HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));   // nrec, nlong
         if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
-        if (c->remit)                  // the record log of k_agg's pass 2 first (nrec = nemit)
+        if (c->remit && c->two_pass_used)   // the record log of pass 2 first (nrec = nemit; only
+                                            // two-pass map calls write it)
             k_copy_emit<<<(unsigned)(c->ncu * 4), 256, 0, c->stream>>>(
                 c->remit, c->recA, std::min<u64>(c->rec_cap, emit_cap), c->st);
         k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
@@ -860,21 +861,28 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // k_agg read k_map's outputs only and share nothing but atomic counters (the record log's
     // cursor, the global table's claim protocol), and both are latency-bound (C4 1 GiB: 1.7 ms of
     // long-key work beside 3.2 ms of aggregation)
+    // Only two-pass (high-cardinality) jobs fork: on low-cardinality text the long-key kernels
+    // take ~25 us and could not run beside k_agg anyway (its workgroups fill every CU's LDS),
+    // while the fork and join cost ~25 us of dependency latency.
     const bool long_path = ablate == 0 || ablate >= 6;
-    if (long_path) {
+    const bool fork = long_path && two_pass;
+    hipStream_t ls = fork ? c->long_stream : c->stream;
+    if (fork) {
         HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
         HIPCHK(c, hipStreamWaitEvent(c->long_stream, c->ev_fork, 0));
+    }
+    if (long_path) {
         LongPart lp;
         const u64 expect = grid * (u64)a.tiles_per_wg * 16;     // 16 per step: 3x C4's rate
         lp.cap = (u32)std::min<u64>(std::max<u64>(1024, (expect * 5 / 4 + LQ - 1) / LQ), 0x7FFFFFFFull);
         RC(ensure(c, &c->lent, &c->lent_cap, (u64)LQ * lp.cap));
         RC(ensure(c, &c->lpcur, &c->lpcur_cap, (u64)LQ));
-        HIPCHK(c, hipMemsetAsync(c->lpcur, 0, LQ * sizeof(u32), c->long_stream));
+        HIPCHK(c, hipMemsetAsync(c->lpcur, 0, LQ * sizeof(u32), ls));
         lp.ent = c->lent; lp.cur = c->lpcur;
-        k_long_hash<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, c->long_stream>>>(a, lp, (u32)grid);
-        k_long_agg<<<LQ, LONG_NT, 0, c->long_stream>>>(a, lp);
+        k_long_hash<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, ls>>>(a, lp, (u32)grid);
+        k_long_agg<<<LQ, LONG_NT, 0, ls>>>(a, lp);
         HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipEventRecord(c->ev_join, c->long_stream));
+        if (fork) HIPCHK(c, hipEventRecord(c->ev_join, c->long_stream));
     }
     // k_agg pass 1 (spills what its LDS tables cannot hold) -> k_rp -> pass 2 (wcg_agg.h)
     AggArgs g;
@@ -919,7 +927,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     k_agg<AGG_EMIT><<<grid2, AGG_NT, 0, c->stream>>>(g2);
     HIPCHK(c, hipGetLastError());
     }
-    if (long_path) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    if (fork) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     if (c->timing) {
         e2 = take_event(c);
         HIPCHK(c, hipEventRecord(e2, c->stream));
