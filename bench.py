@@ -182,11 +182,11 @@ def main():
     work = torch.cuda.Stream()
     torch.cuda.set_stream(work)
     stream = work.cuda_stream
-    # table capacity: the vocabulary, but no more keys than one per 32 input bytes (C4's densest
+    # table capacity: twice the vocabulary, but no more keys than one per 32 input bytes (C4's densest
     # slice has one distinct key per 45 bytes).  Oversized tables cost time: k_compact scans every
     # slot, and the table probes of k_agg/k_long spread over more pages (TLB) and miss the
     # 256 MB MALL.  A table too small for the input fails loudly (WCG_EFULL), never silently.
-    keys_cap = max(min(4 * cfg["vocab"], n // 32), 1 << 18)
+    keys_cap = max(min(2 * cfg["vocab"], n // 32), 1 << 18)
     eng = wcg.Engine(device=local, max_input_bytes=0, max_keys=keys_cap)
     eng.set_stream(stream)
     # HIP events around every kernel phase of every job, summed by the engine and read once after
