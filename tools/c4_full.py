@@ -1,9 +1,8 @@
 #!/usr/bin/env python3
 """BASELINE config 4 at full size on one MI355X: 64 GiB of mixed-script UTF-8 (Zipf s = 0.9 over
-a 5e7-word vocabulary, seed 44), resident in HBM, counted as ONE word-count job - 16 DoMap calls
-(wcg_map_device, 4 GiB each; --call-gib 1: 64 calls; generator blocks end in '\\n', so every call
-is a whole split) into
-one context sized for 5e7 keys, then DoReduce + Merge (wcg_reduce) - and the merged file checked
+a 5e7-word vocabulary, seed 44), resident in HBM, counted as ONE word-count job - 8 DoMap calls
+(wcg_map_device, 8 GiB each; --call-gib 1: 64 calls; generator blocks end in '\\n', so every call
+is a whole split) into one context sized for 5e7 keys, then DoReduce + Merge (wcg_reduce) - and the merged file checked
 exactly against the input by the oracle's verifier (oracle/wc_oracle.c wco_verify_merged: every
 input token decrements its line's count; all counts must end at 0, keys strictly ascending).
 
@@ -33,7 +32,7 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=int, default=64)
-    ap.add_argument("--call-gib", type=int, default=4)
+    ap.add_argument("--call-gib", type=int, default=8)
     ap.add_argument("--jobs", type=int, default=2, help="timed jobs (after one untimed)")
     ap.add_argument("--max-keys", type=int, default=50_000_000)
     ap.add_argument("--threads", type=int, default=16)
