@@ -723,10 +723,12 @@ int wcg_reset(wcg_ctx* c) {
         }
     }
     c->map_launches_since_reset = 0;
-    if (clear_g) HIPCHK(c, hipMemsetAsync(c->gtab, 0, c->gslots * sizeof(GEntry), c->stream));
+    // one launch clears the tables and the counters (three memsets were three dispatches)
+    const u64 g16 = clear_g ? c->gslots * sizeof(GEntry) / 16 : 0, l16 = c->lslots * sizeof(GEntry) / 16;
+    k_clear<<<grid_for(g16 + l16, 256, c->ncu * 4), 256, 0, c->stream>>>(
+        reinterpret_cast<uint4*>(c->gtab), g16, reinterpret_cast<uint4*>(c->ltab), l16, c->st);
+    HIPCHK(c, hipGetLastError());
     c->gtab_zero = true;
-    HIPCHK(c, hipMemsetAsync(c->ltab, 0, c->lslots * sizeof(GEntry), c->stream));
-    HIPCHK(c, hipMemsetAsync(c->st, 0, sizeof(DevState), c->stream));
     c->compacted = c->reduced = false;
     c->exp_ready = false;
     c->part_R = 0;

@@ -87,6 +87,19 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
         if (have & (1u << j)) { if (pos < cap) out[pos] = r[j]; pos++; }   // more: host grows, reruns
 }
 
+// wcg_reset: zero n1 + n2 16-byte words of two tables and the DevState counters, one dispatch
+__global__ void k_clear(uint4* t1, u64 n1, uint4* t2, u64 n2, DevState* st) {
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n1 + n2; i += stride) {
+        if (i < n1) t1[i] = z; else t2[i - n1] = z;
+    }
+    if (blockIdx.x == 0) {
+        u32* w = reinterpret_cast<u32*>(st);
+        for (u32 k = threadIdx.x; k < sizeof(DevState) / 4; k += blockDim.x) w[k] = 0;
+    }
+}
+
 // two-pass jobs compact into the record log itself: the tables' records follow its
 // min(nemit, cap) records
 __global__ void k_log_len(u64 cap, DevState* st) {
