@@ -157,6 +157,32 @@ WCG_API int wcg_import(wcg_ctx *ctx, const void *dev_records, uint64_t nrecords)
 WCG_API int wcg_export_count(wcg_ctx *ctx, uint32_t nreduce, uint32_t nranks, uint64_t *counts);
 WCG_API int wcg_export_write(wcg_ctx *ctx, void *dev_dst);
 
+/* ---- the shuffle and the final Merge inside the library, over RCCL (one process per GPU) ----
+ * The reference moves partitions between its phases as files: DoMap writes mrtmp.<f>-<m>-<r>
+ * for r = ihash(key) % nReduce (mapreduce.go:214-230), DoReduce r reads partition r of every
+ * map job (mapreduce.go:242-263), Merge reads every -res-<r> (mapreduce.go:284-321).  On one
+ * node of GPUs these hand-offs are RCCL collectives over xGMI on the context's stream:
+ *   wcg_comm_id      ncclGetUniqueId: made on rank 0, handed to every rank by the host (the
+ *                    config-5 master RPC, torch.distributed, a file - 128 opaque bytes)
+ *   wcg_comm_init    ncclCommInitRank for this context (world may be 1)
+ *   wcg_exchange     export the local aggregate by owner = (ihash % nreduce) % world into a send
+ *                    buffer, ncclAllToAll the unit counts, ONE host read of them, grouped
+ *                    ncclSend/ncclRecv of the 32-byte units, then this context keeps exactly the
+ *                    keys of the partitions it owns (tables cleared, received units imported).
+ *                    All device work is ordered on the context's stream; *sent / *received =
+ *                    units (may be NULL).  Follow with wcg_reduce (DoReduce of the owned
+ *                    partitions: sorted "key: count" run of this rank).
+ *   wcg_gather_merge after wcg_reduce on every rank: every rank's sorted run goes to `root`
+ *                    (ncclAllGather of the run sizes, one host read, ncclSend/ncclRecv), which
+ *                    merges the runs on its GPU (as wcg_merge_runs) into its result.  On root
+ *                    *nkeys / *nbytes describe the merged file; elsewhere they are 0.
+ * Collective calls: every rank of the communicator makes them in the same order. */
+#define WCG_COMM_ID_BYTES 128
+WCG_API int wcg_comm_id(uint8_t *id_out /* WCG_COMM_ID_BYTES */);
+WCG_API int wcg_comm_init(wcg_ctx *ctx, const uint8_t *id /* WCG_COMM_ID_BYTES */, int rank, int world);
+WCG_API int wcg_exchange(wcg_ctx *ctx, uint32_t nreduce, uint64_t *sent, uint64_t *received);
+WCG_API int wcg_gather_merge(wcg_ctx *ctx, int root, uint64_t *nkeys, uint64_t *nbytes);
+
 /* Merge (mapreduce.go:284-321) of sorted runs: dev_text holds nruns formatted outputs back to
  * back (each a sorted "key: count\n" file, e.g. the wcg_reduce output of every owner rank, with
  * disjoint keys), run r being run_bytes[r] bytes.  The runs are merged pairwise on the device
@@ -169,7 +195,10 @@ WCG_API int wcg_merge_runs(wcg_ctx *ctx, const void *dev_text, const uint64_t *r
  * on the context's stream: ms[0] map kernel (tokenize + LDS aggregation, summed over the
  * wcg_map* calls since wcg_reset), ms[1] long-token counting + miss-log aggregation kernels
  * (k_long_hash, k_long_agg, k_agg pass 1, k_rp, k_agg pass 2), ms[2] compaction,
- * ms[3] sort, ms[4] format.  n = number of doubles the caller provides (<= 5). */
+ * ms[3] sort, ms[4] format; the shuffle of wcg_exchange: ms[5] export (counts + unit writes),
+ * ms[6] RCCL exchange (counts all-to-all, its host read, grouped send/recv), ms[7] import;
+ * wcg_gather_merge: ms[8] RCCL gather of the runs to root, ms[9] merge of the runs.
+ * n = number of doubles the caller provides (<= 10). */
 WCG_API int wcg_timings(wcg_ctx *ctx, double *ms, int n, uint64_t *map_launches);
 /* Enable/disable the event timing above (off by default: it adds event records).  on = 1: the
  * phases of the last job; on = 2: every job from this call on, summed (wcg_reset keeps the events,

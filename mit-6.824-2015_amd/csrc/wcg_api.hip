@@ -5,6 +5,7 @@
 // aggregation tables, the record buffers for the sort and the formatted output all stay
 // resident, so a job is a fixed sequence of launches on one stream.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -18,6 +19,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/wcg.h"
@@ -87,7 +89,17 @@ struct wcg_ctx {
     Rec* exp_buf = nullptr; u64 exp_cap = 0;
     // merge of formatted runs
     u64* nlpos = nullptr; u64 nlpos_cap = 0;
-    u64* d_rb = nullptr; u64* d_b0 = nullptr; u64 rb_cap = 0;
+    u64* d_rb = nullptr; u64 rb_cap = 0;
+    u64* d_b0 = nullptr; u64 b0_cap = 0;
+    bool merged = false;                      // the result is a merge of runs (wcg_merge_runs): the
+                                              // sorted records are line records, not keys
+    // RCCL shuffle (wcg_comm_init / wcg_exchange / wcg_gather_merge)
+    ncclComm_t comm = nullptr;
+    int comm_rank = 0, comm_world = 0;
+    u64* d_xcnt = nullptr;                    // [4 * EX_MAX_RANKS]: received unit counts, run sizes
+    u64* h_xcnt = nullptr;                    // pinned [4 * EX_MAX_RANKS]
+    Rec* xrecv = nullptr; u64 xrecv_cap = 0;  // received units
+    uint8_t* grecv = nullptr; u64 grecv_cap = 0;   // root: the gathered runs
     u64* h_rb = nullptr; u64 h_rb_cap = 0;    // pinned run bounds
     // per-occurrence JSON map output (wcg_map_json)
     uint8_t* d_jin = nullptr; u64 jin_cap = 0;
@@ -121,6 +133,9 @@ struct wcg_ctx {
     int timing_mode = 0;                     // 1: the last job; 2: every job since enable (no reads in between)
     std::vector<std::array<hipEvent_t, 5>> phase_jobs;   // mode 2: each job's phase events
     bool phase_rec = false;
+    // shuffle phases (wcg_timings ms[5..9]): {phase, start, end}
+    std::vector<std::tuple<int, hipEvent_t, hipEvent_t>> xev;
+    double acc[10] = {};                      // mode 2: phases folded in from recycled events
     u64 map_launches = 0;
     std::string err;
 };
@@ -674,8 +689,11 @@ int wcg_close(wcg_ctx* c) {
     void* bufs[] = {c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens, c->d_scalar, c->d_out,
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
                     c->llog, c->llog_len, c->smp, c->bid, c->spx, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->ovf, c->hist, c->spart, c->ikey, c->iidx, c->groups,
-                    c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig};
+                    c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig,
+                    c->d_xcnt, c->xrecv, c->grecv};
+    if (c->comm) (void)ncclCommDestroy(c->comm);
     for (void* b : bufs) if (b) (void)hipFree(b);
+    if (c->h_xcnt) (void)hipHostFree(c->h_xcnt);
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->h_scalar) (void)hipHostFree(c->h_scalar);
     if (c->h_cur) (void)hipHostFree(c->h_cur);
@@ -689,7 +707,20 @@ int wcg_close(wcg_ctx* c) {
 
 int wcg_set_stream(wcg_ctx* c, void* stream) {
     if (!c) return WCG_EINVAL;
-    c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    hipStream_t next = stream ? (hipStream_t)stream : c->own_stream;
+    if (next != c->stream) {
+        // work already queued on the old stream (wcg_open's table clear, a reset that the next
+        // reset will assume done) is ordered before anything queued on the new one
+        int rc = set_dev(c);
+        if (rc) return rc;
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        hipError_t r1 = hipEventRecord(e, c->stream);
+        hipError_t r2 = r1 == hipSuccess ? hipStreamWaitEvent(next, e, 0) : r1;
+        (void)hipEventDestroy(e);
+        HIPCHK(c, r2);
+        c->stream = next;
+    }
     return WCG_OK;
 }
 
@@ -698,16 +729,53 @@ int wcg_enable_timing(wcg_ctx* c, int on) {
     c->timing = on != 0;
     c->timing_mode = on == 2 ? 2 : (on ? 1 : 0);
     if (c->timing_mode == 2) {           // a new accumulation epoch
-        c->map_ev.clear(); c->agg_ev.clear(); c->phase_jobs.clear();
+        c->map_ev.clear(); c->agg_ev.clear(); c->phase_jobs.clear(); c->xev.clear();
         c->ev_used = 0; c->map_launches = 0; c->phase_rec = false;
+        for (double& v : c->acc) v = 0;
     }
     return WCG_OK;
 }
 
-int wcg_reset(wcg_ctx* c) {
-    if (!c) return WCG_EINVAL;
-    int rc = set_dev(c);
-    if (rc) return rc;
+}  // extern "C"
+
+namespace {
+
+// timing mode 2 keeps every job's events until wcg_timings; past this many events the pending
+// pairs are folded into c->acc (one host wait every few hundred jobs) and the events reused
+constexpr size_t EV_FOLD = 4096;
+
+double ev_ms(hipEvent_t a, hipEvent_t b) {
+    float f = 0;
+    if (!a || !b || hipEventElapsedTime(&f, a, b) != hipSuccess) return 0.0;
+    return f;
+}
+
+// every recorded phase pair added to acc[] (the caller has synchronised the stream)
+void sum_events(const wcg_ctx* c, double* acc) {
+    for (auto& p : c->map_ev) acc[0] += ev_ms(p.first, p.second);
+    for (auto& p : c->agg_ev) acc[1] += ev_ms(p.first, p.second);
+    for (auto& j : c->phase_jobs) {
+        acc[2] += ev_ms(j[0], j[1]);
+        acc[3] += ev_ms(j[2], j[3]);
+        acc[4] += ev_ms(j[3], j[4]);
+    }
+    for (auto& x : c->xev) acc[std::get<0>(x)] += ev_ms(std::get<1>(x), std::get<2>(x));
+}
+
+void record_x(wcg_ctx* c, int phase, hipEvent_t a, hipEvent_t b) {
+    if (c->timing && a && b) c->xev.emplace_back(phase, a, b);
+}
+
+hipEvent_t mark(wcg_ctx* c) {
+    if (!c->timing) return nullptr;
+    hipEvent_t e = take_event(c);
+    return hipEventRecord(e, c->stream) == hipSuccess ? e : nullptr;
+}
+
+// a new job's tables: clear what may have been written since the last clear, reset the job state
+// (wcg_reset; wcg_exchange before it imports the partitions this rank owns - the job's timing
+// events are kept there)
+int reset_tables(wcg_ctx* c) {
     // The global table (up to GBs) is cleared only if something may have written it since it was
     // last cleared: every kernel that inserts into it counts global_ops, and wcg_import sets
     // `imported`; two-pass jobs normally leave it empty.
@@ -729,20 +797,39 @@ int wcg_reset(wcg_ctx* c) {
         reinterpret_cast<uint4*>(c->gtab), g16, reinterpret_cast<uint4*>(c->ltab), l16, c->st);
     HIPCHK(c, hipGetLastError());
     c->gtab_zero = true;
-    c->compacted = c->reduced = false;
+    c->compacted = c->reduced = c->merged = false;
     c->exp_ready = false;
     c->part_R = 0;
     c->nrec = 0;
     c->out_len = 0;
+    c->two_pass_used = false;
+    c->imported = false;
+    return WCG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wcg_reset(wcg_ctx* c) {
+    if (!c) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    if (c->timing_mode == 2 && c->ev_used >= EV_FOLD) {   // recycle the events of earlier jobs
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        sum_events(c, c->acc);
+        c->map_ev.clear(); c->agg_ev.clear(); c->phase_jobs.clear(); c->xev.clear();
+        c->ev_used = 0;
+    }
+    RC(reset_tables(c));
     if (c->timing_mode != 2) {          // mode 2 keeps every job's events until wcg_timings
         c->map_ev.clear();
         c->agg_ev.clear();
+        c->xev.clear();
         c->ev_used = 0;
         c->phase_rec = false;
         c->map_launches = 0;
     }
-    c->two_pass_used = false;
-    c->imported = false;
     return WCG_OK;
 }
 
@@ -840,6 +927,13 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     a.pool = c->pool;
     a.region_len = c->region_len;
     a.wg_stats = c->wg_stats;
+    a.stamps = nullptr;
+#if WCG_STAMPS
+    static u64* d_stamps = nullptr;
+    if (!d_stamps) HIPCHK(c, hipMalloc(&d_stamps, MAP_NSTAMP * sizeof(u64)));
+    HIPCHK(c, hipMemsetAsync(d_stamps, 0, MAP_NSTAMP * sizeof(u64), c->stream));
+    a.stamps = d_stamps;
+#endif
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (c->timing) { e0 = take_event(c); HIPCHK(c, hipEventRecord(e0, c->stream)); }
     static const int ablate = getenv("WCG_MAP_ABLATE") ? atoi(getenv("WCG_MAP_ABLATE")) : 0;
@@ -854,6 +948,17 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         default: k_map<0><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
     }
     HIPCHK(c, hipGetLastError());
+#if WCG_STAMPS
+    {   // diagnostics: cycles per step and phase, averaged over every wave's steps
+        u64 h[MAP_NSTAMP];
+        HIPCHK(c, hipMemcpyAsync(h, d_stamps, sizeof h, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const double ns = h[6] ? (double)h[6] : 1.0;
+        fprintf(stderr, "wcg stamps (s_memtime ticks per wave step, %llu steps): loop %.0f wait %.0f mask %.0f "
+                "list %.0f short %.0f general %.0f\n", (unsigned long long)h[6], h[0] / ns, h[1] / ns, h[2] / ns,
+                h[3] / ns, h[4] / ns, h[5] / ns);
+    }
+#endif
     if (c->timing) { e1 = take_event(c); HIPCHK(c, hipEventRecord(e1, c->stream)); }
     // the logged long tokens: hashed into LQ partitions (LONG_PARTS workgroups per map
     // workgroup's region), then one workgroup per partition.  Partition capacity: the log's
@@ -938,7 +1043,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     }
     c->map_launches++;
     c->map_launches_since_reset++;
-    c->compacted = c->reduced = false;
+    c->compacted = c->reduced = c->merged = false;
     c->exp_ready = false;
     c->part_R = 0;
     return WCG_OK;
@@ -983,7 +1088,9 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
     if (!c) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
+    c->phase_ev[0] = c->phase_ev[1] = nullptr;     // set by compact() only when it runs now
     RC(compact(c));
+    c->merged = false;
     if (c->timing) { c->phase_ev[2] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream)); }
     RC(sort_records(c));
     if (c->timing) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }
@@ -1071,6 +1178,7 @@ int wcg_sync(wcg_ctx* c) {
 int wcg_partition_all(wcg_ctx* c, uint32_t nreduce, uint8_t* host_out, uint64_t cap, uint64_t* part_bytes) {
     if (!c) return WCG_EINVAL;
     if (!c->reduced) { c->err = "wcg_partition_all before wcg_reduce"; return WCG_ESTATE; }
+    if (c->merged) { c->err = "wcg_partition_all after wcg_merge_runs (a merged file has no partitions)"; return WCG_ESTATE; }
     if (nreduce == 0) { c->err = "wcg_partition_all: nreduce 0"; return WCG_EINVAL; }
     int rc = set_dev(c);
     if (rc) return rc;
@@ -1093,6 +1201,7 @@ int wcg_partition_all(wcg_ctx* c, uint32_t nreduce, uint8_t* host_out, uint64_t 
 int wcg_partition(wcg_ctx* c, uint32_t nreduce, uint32_t r, uint8_t* host_out, uint64_t cap, uint64_t* nbytes) {
     if (!c) return WCG_EINVAL;
     if (!c->reduced) { c->err = "wcg_partition before wcg_reduce"; return WCG_ESTATE; }
+    if (c->merged) { c->err = "wcg_partition after wcg_merge_runs (a merged file has no partitions)"; return WCG_ESTATE; }
     if (nreduce == 0 || r >= nreduce) { c->err = "wcg_partition: bad partition"; return WCG_EINVAL; }
     int rc = set_dev(c);
     if (rc) return rc;
@@ -1113,6 +1222,7 @@ int wcg_partition(wcg_ctx* c, uint32_t nreduce, uint32_t r, uint8_t* host_out, u
 
 int wcg_export_count(wcg_ctx* c, uint32_t nreduce, uint32_t nranks, uint64_t* counts) {
     if (!c || !counts || nreduce == 0 || nranks == 0 || nranks > EX_MAX_RANKS) return WCG_EINVAL;
+    if (c->merged) { c->err = "wcg_export after wcg_merge_runs"; return WCG_ESTATE; }
     int rc = set_dev(c);
     if (rc) return rc;
     RC(compact(c));
@@ -1173,7 +1283,7 @@ int wcg_import(wcg_ctx* c, const void* dev_records, uint64_t nrecords) {
                                                                           c->arena, c->arena_cap, c->st);
     HIPCHK(c, hipGetLastError());
     c->imported = true;
-    c->compacted = c->reduced = false;
+    c->compacted = c->reduced = c->merged = false;
     c->exp_ready = false;
     c->part_R = 0;
     return WCG_OK;          // a full table is reported by the next wcg_reduce / wcg_export_count
@@ -1191,7 +1301,7 @@ int wcg_merge_runs(wcg_ctx* c, const void* dev_text, const uint64_t* run_bytes, 
     c->part_R = 0;
     c->reduced = false;
     if (total == 0) {
-        c->nrec = 0; c->nkeys = 0; c->out_len = 0; c->reduced = true;
+        c->nrec = 0; c->nkeys = 0; c->out_len = 0; c->reduced = true; c->merged = true;
         if (nkeys) *nkeys = 0;
         if (nbytes) *nbytes = 0;
         return WCG_OK;
@@ -1221,7 +1331,7 @@ int wcg_merge_runs(wcg_ctx* c, const void* dev_text, const uint64_t* run_bytes, 
         c->h_rb_cap = nruns + 1;
     }
     RC(ensure(c, &c->d_rb, &c->rb_cap, nruns + 1));
-    RC(ensure(c, &c->d_b0, &c->rb_cap, nruns + 1));
+    RC(ensure(c, &c->d_b0, &c->b0_cap, nruns + 1));
     u64 acc = 0;
     for (u32 r = 0; r <= nruns; r++) { c->h_rb[r] = acc; if (r < nruns) acc += run_bytes[r]; }
     HIPCHK(c, hipMemcpyAsync(c->d_rb, c->h_rb, (nruns + 1) * sizeof(u64), hipMemcpyHostToDevice, c->stream));
@@ -1245,6 +1355,7 @@ int wcg_merge_runs(wcg_ctx* c, const void* dev_text, const uint64_t* run_bytes, 
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->h_st->bad_input) { c->err = "wcg_merge_runs: a line is not \"key: count\""; return WCG_EINVAL; }
     c->reduced = true;
+    c->merged = true;
     if (nkeys) *nkeys = L;
     if (nbytes) *nbytes = c->out_len;
     return WCG_OK;
@@ -1285,27 +1396,187 @@ int wcg_map_json(wcg_ctx* c, const uint8_t* host_bytes, uint64_t n, uint32_t nre
     return WCG_OK;
 }
 
+// ---------------------------------------------------------------- RCCL shuffle and Merge
+#define NCCLCHK(ctx, call)                                                                  \
+    do {                                                                                    \
+        ncclResult_t r_ = (call);                                                           \
+        if (r_ != ncclSuccess) {                                                            \
+            (ctx)->err = std::string(#call) + ": " + ncclGetErrorString(r_);                \
+            return WCG_EHIP;                                                                \
+        }                                                                                   \
+    } while (0)
+
+int wcg_comm_id(uint8_t* id_out) {
+    if (!id_out) return WCG_EINVAL;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return WCG_EHIP;
+    static_assert(sizeof(u.internal) == WCG_COMM_ID_BYTES, "ncclUniqueId size");
+    memcpy(id_out, u.internal, WCG_COMM_ID_BYTES);
+    return WCG_OK;
+}
+
+int wcg_comm_init(wcg_ctx* c, const uint8_t* id, int rank, int world) {
+    if (!c) return WCG_EINVAL;
+    if (!id || world < 1 || (u32)world > EX_MAX_RANKS || rank < 0 || rank >= world) {
+        c->err = "wcg_comm_init: bad rank / world";
+        return WCG_EINVAL;
+    }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
+    if (!c->d_xcnt) {
+        HIPCHK(c, hipMalloc(&c->d_xcnt, 4 * EX_MAX_RANKS * sizeof(u64)));
+        HIPCHK(c, hipHostMalloc(&c->h_xcnt, 4 * EX_MAX_RANKS * sizeof(u64), hipHostMallocDefault));
+    }
+    ncclUniqueId u;
+    memcpy(u.internal, id, WCG_COMM_ID_BYTES);
+    NCCLCHK(c, ncclCommInitRank(&c->comm, world, u, rank));
+    c->comm_rank = rank;
+    c->comm_world = world;
+    return WCG_OK;
+}
+
+// The shuffle of mapreduce.go:214-230 / 242-263 between the GPUs of one job: every rank's
+// aggregate leaves as 32-byte units bucketed by owner rank and the owner imports what it
+// receives.  Stream order: compaction -> k_export_count -> ncclAllToAll(unit counts) -> [the one
+// host read: send and receive counts] -> k_export_write into the send buffer -> grouped
+// ncclSend/ncclRecv -> table clear -> k_import.
+int wcg_exchange(wcg_ctx* c, uint32_t nreduce, uint64_t* sent, uint64_t* received) {
+    if (!c) return WCG_EINVAL;
+    if (!c->comm) { c->err = "wcg_exchange before wcg_comm_init"; return WCG_ESTATE; }
+    if (nreduce == 0) { c->err = "wcg_exchange: nreduce 0"; return WCG_EINVAL; }
+    if (c->merged) { c->err = "wcg_exchange after wcg_merge_runs"; return WCG_ESTATE; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    const u32 W = (u32)c->comm_world;
+    hipEvent_t e0 = mark(c);
+    RC(compact(c));
+    const u64 n = c->nrec;
+    RC(ensure(c, &c->owner, &c->owner_cap, n + 1));
+    HIPCHK(c, hipMemsetAsync(c->d_per_rank, 0, W * sizeof(u64), c->stream));
+    if (n) {
+        k_export_count<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(c->crec, n, nreduce, W, c->arena,
+                                                                            c->owner, c->d_per_rank);
+        HIPCHK(c, hipGetLastError());
+    }
+    NCCLCHK(c, ncclAllToAll(c->d_per_rank, c->d_xcnt, 1, ncclUint64, c->comm, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_xcnt, c->d_per_rank, W * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_xcnt + EX_MAX_RANKS, c->d_xcnt, W * sizeof(u64), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));     // the one host read of the exchange
+    const u64* scnt = c->h_xcnt;
+    const u64* rcnt = c->h_xcnt + EX_MAX_RANKS;
+    u64* soff = c->h_xcnt + 2 * EX_MAX_RANKS;       // send offsets (also the export cursors)
+    u64* roff = c->h_xcnt + 3 * EX_MAX_RANKS;
+    u64 ts = 0, tr = 0;
+    for (u32 p = 0; p < W; p++) { soff[p] = ts; ts += scnt[p]; roff[p] = tr; tr += rcnt[p]; }
+    RC(ensure(c, &c->exp_buf, &c->exp_cap, ts + 1));
+    RC(ensure(c, &c->xrecv, &c->xrecv_cap, tr + 1));
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(c->d_per_rank + EX_MAX_RANKS, soff, W * sizeof(u64), hipMemcpyHostToDevice,
+                                 c->stream));
+        k_export_write<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(
+            c->crec, n, W, c->owner, c->d_per_rank + EX_MAX_RANKS, c->arena, c->exp_buf);
+        HIPCHK(c, hipGetLastError());
+    }
+    hipEvent_t e1 = mark(c);
+    NCCLCHK(c, ncclGroupStart());
+    for (u32 p = 0; p < W; p++) {
+        if (scnt[p])
+            NCCLCHK(c, ncclSend(c->exp_buf + soff[p], scnt[p] * sizeof(Rec), ncclUint8, (int)p, c->comm, c->stream));
+        if (rcnt[p])
+            NCCLCHK(c, ncclRecv(c->xrecv + roff[p], rcnt[p] * sizeof(Rec), ncclUint8, (int)p, c->comm, c->stream));
+    }
+    NCCLCHK(c, ncclGroupEnd());
+    hipEvent_t e2 = mark(c);
+    // this rank now holds exactly its own partitions
+    RC(reset_tables(c));
+    if (tr) {
+        k_import<<<grid_for(tr, 256, c->ncu * 8), 256, 0, c->stream>>>(c->xrecv, tr, c->gtab, c->gslots - 1, c->ltab,
+                                                                      c->lslots - 1, c->arena, c->arena_cap, c->st);
+        HIPCHK(c, hipGetLastError());
+        c->imported = true;
+    }
+    hipEvent_t e3 = mark(c);
+    record_x(c, 5, e0, e1);
+    record_x(c, 6, e1, e2);
+    record_x(c, 7, e2, e3);
+    if (sent) *sent = ts;
+    if (received) *received = tr;
+    return WCG_OK;
+}
+
+// Merge (mapreduce.go:284-321) across the ranks: the owners' sorted runs (disjoint key sets)
+// travel to root, which merges them without a re-sort (wcg_merge_runs).
+int wcg_gather_merge(wcg_ctx* c, int root, uint64_t* nkeys, uint64_t* nbytes) {
+    if (!c) return WCG_EINVAL;
+    if (!c->comm) { c->err = "wcg_gather_merge before wcg_comm_init"; return WCG_ESTATE; }
+    if (root < 0 || root >= c->comm_world) { c->err = "wcg_gather_merge: bad root"; return WCG_EINVAL; }
+    if (!c->reduced || c->merged) { c->err = "wcg_gather_merge needs a wcg_reduce result"; return WCG_ESTATE; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    const u32 W = (u32)c->comm_world;
+    const bool am_root = c->comm_rank == root;
+    hipEvent_t e0 = mark(c);
+    u64* d_mine = c->d_xcnt + 2 * EX_MAX_RANKS;
+    u64* d_all = c->d_xcnt + 3 * EX_MAX_RANKS;
+    c->h_xcnt[2 * EX_MAX_RANKS] = c->out_len;
+    HIPCHK(c, hipMemcpyAsync(d_mine, c->h_xcnt + 2 * EX_MAX_RANKS, sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(c, ncclAllGather(d_mine, d_all, 1, ncclUint64, c->comm, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_xcnt, d_all, W * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));     // the run sizes (one host read)
+    std::vector<uint64_t> sizes(c->h_xcnt, c->h_xcnt + W);
+    u64 total = 0;
+    for (uint64_t s : sizes) total += s;
+    if (!am_root) {
+        if (c->out_len)
+            NCCLCHK(c, ncclSend(c->d_out, c->out_len, ncclUint8, root, c->comm, c->stream));
+        hipEvent_t e1 = mark(c);
+        record_x(c, 8, e0, e1);
+        if (nkeys) *nkeys = 0;
+        if (nbytes) *nbytes = 0;
+        return WCG_OK;
+    }
+    RC(ensure(c, &c->grecv, &c->grecv_cap, total + 64));
+    u64 off = 0;
+    NCCLCHK(c, ncclGroupStart());
+    for (u32 p = 0; p < W; p++) {
+        if (sizes[p] && (int)p != root)
+            NCCLCHK(c, ncclRecv(c->grecv + off, sizes[p], ncclUint8, (int)p, c->comm, c->stream));
+        off += sizes[p];
+    }
+    NCCLCHK(c, ncclGroupEnd());
+    off = 0;
+    for (u32 p = 0; p < (u32)root; p++) off += sizes[p];
+    if (sizes[root]) HIPCHK(c, hipMemcpyAsync(c->grecv + off, c->d_out, sizes[root], hipMemcpyDeviceToDevice, c->stream));
+    hipEvent_t e1 = mark(c);
+    RC(wcg_merge_runs(c, c->grecv, sizes.data(), W, nkeys, nbytes));
+    hipEvent_t e2 = mark(c);
+    record_x(c, 8, e0, e1);
+    record_x(c, 9, e1, e2);
+    return WCG_OK;
+}
+
 int wcg_timings(wcg_ctx* c, double* ms, int n, uint64_t* map_launches) {
     if (!c || !ms || n < 0) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    double v[5] = {0, 0, 0, 0, 0};
-    float f = 0;
-    for (auto& p : c->map_ev) { HIPCHK(c, hipEventElapsedTime(&f, p.first, p.second)); v[0] += f; }
-    for (auto& p : c->agg_ev) { HIPCHK(c, hipEventElapsedTime(&f, p.first, p.second)); v[1] += f; }
-    if (c->timing_mode == 2) {          // summed over every job of the epoch
-        for (auto& j : c->phase_jobs) {
-            HIPCHK(c, hipEventElapsedTime(&f, j[0], j[1])); v[2] += f;
-            HIPCHK(c, hipEventElapsedTime(&f, j[2], j[3])); v[3] += f;
-            HIPCHK(c, hipEventElapsedTime(&f, j[3], j[4])); v[4] += f;
+    double v[10] = {};
+    if (c->timing_mode == 2) {          // summed over every job of the epoch (folded ones too)
+        for (int i = 0; i < 10; i++) v[i] = c->acc[i];
+        sum_events(c, v);
+    } else {
+        for (auto& p : c->map_ev) v[0] += ev_ms(p.first, p.second);
+        for (auto& p : c->agg_ev) v[1] += ev_ms(p.first, p.second);
+        if (c->phase_rec) {
+            v[2] = ev_ms(c->phase_ev[0], c->phase_ev[1]);
+            v[3] = ev_ms(c->phase_ev[2], c->phase_ev[3]);
+            v[4] = ev_ms(c->phase_ev[3], c->phase_ev[4]);
         }
-    } else if (c->phase_rec) {
-        HIPCHK(c, hipEventElapsedTime(&f, c->phase_ev[0], c->phase_ev[1])); v[2] = f;
-        HIPCHK(c, hipEventElapsedTime(&f, c->phase_ev[2], c->phase_ev[3])); v[3] = f;
-        HIPCHK(c, hipEventElapsedTime(&f, c->phase_ev[3], c->phase_ev[4])); v[4] = f;
+        for (auto& x : c->xev) v[std::get<0>(x)] += ev_ms(std::get<1>(x), std::get<2>(x));
     }
-    for (int i = 0; i < n && i < 5; i++) ms[i] = v[i];
+    for (int i = 0; i < n && i < 10; i++) ms[i] = v[i];
     if (map_launches) *map_launches = c->map_launches;
     return WCG_OK;
 }

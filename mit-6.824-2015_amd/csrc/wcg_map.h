@@ -73,6 +73,11 @@ constexpr int MAP_SETS = WCG_MAP_SETS;       // steps in flight per wave (2 or 4
 #ifndef WCG_NOWAIT
 #define WCG_NOWAIT 0                         // diagnostics: 1 = never wait for the window loads
 #endif
+#ifndef WCG_STAMPS
+#define WCG_STAMPS 0                         // diagnostics: s_memtime cycles per k_map phase
+#endif
+constexpr int MAP_NSTAMP = 7;                // {loop, window wait, staging+mask, start list, short loop,
+                                             //  general loop, steps}
 constexpr int MAX_MISS_BUCKETS = 64;         // miss buckets P (the host uses 64)
 constexpr u32 SST_LEN_SHIFT = 10;            // start entry = window offset | min(run, 16) << 10
 
@@ -94,6 +99,7 @@ struct MapArgs {
     Rec* emit;     u64 emit_cap;    // two-pass jobs: the record log (k_long_hash's inline runs)
     u32 evict_at;                   // WCG_EVICT: after this many steps per wave, the LDS table
     u32 evict_min;                  //   drops entries counted fewer than evict_min times (0: never)
+    u64* stamps;                    // WCG_STAMPS builds: MAP_NSTAMP sums over all waves
 };
 constexpr u64 LLOG_OFF_MASK = (1ull << 40) - 1;   // record = input offset | len << 40 (len 0: walk)
 constexpr u32 LLOG_PER_STEP = 64;                 // long-token log records per step: a bound (a
@@ -559,6 +565,11 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
 
     uint8_t* const bytes = wbytes[wave];
     uint16_t* const sst = wstart[wave];
+    u64 stp[MAP_NSTAMP] = {};                     // WCG_STAMPS: cycles per phase (wave-uniform)
+    u64 t_last = WCG_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int i) {
+        if (WCG_STAMPS) { const u64 t = __builtin_amdgcn_s_memtime(); stp[i] += t - t_last; t_last = t; }
+    };
     // Steps are dealt chip-wide: wave w of workgroup g takes steps (g * 16 + w) + k * G * 16, so
     // the chip sweeps the input front to back (HBM-friendly) while every workgroup still sees
     // a uniform sample of it for its LDS table.
@@ -644,6 +655,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         m = (m | ((u32)__builtin_amdgcn_update_dpp(0, (int)(m >> 16), 0x138, 0xF, 0xF, false) & 7u)) & 0xFFFFu;
         if (ABL == 4) { asm volatile("" ::"v"(m)); return 0; }
         wmask[wave][lane] = (uint16_t)m;
+        stamp(2);
         // neighbours' masks by DPP lane shifts
         const u32 prevm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x138, 0xF, 0xF, false);   // wave_shr:1
         const u32 nextm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x130, 0xF, 0xF, false);   // wave_shl:1
@@ -680,6 +692,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             o_o += sh ? 0u : 1u;
         }
         wave_lds_sync();
+        stamp(3);
         my_tokens += total;
 
         // ---- tokens: uniform iterations of 64 tokens (every lane runs every iteration; lanes
@@ -811,6 +824,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         } else {
             e_nxt = sst[lane];
         }
+        stamp(4);
         if (iters) {
             cur = decode_tok(e_nxt, first + lane < total, keyread(e_nxt));
             e_nxt = sst[first + 64 + lane];
@@ -852,6 +866,8 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         if (ABL == 0 || ABL >= 6) store_pending(true);
         if (ABL) asm volatile("" ::"v"(sink));
         wave_lds_sync();
+        stamp(5);
+        if (WCG_STAMPS) stp[6]++;
         return (ABL == 0 || ABL >= 6) ? nsh + 2 * (iters + 1) + extra_stores : 0u;
     };
 
@@ -902,9 +918,11 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         if (st >= nsteps || is_tail(st)) break;                                                 \
         v4i r; u32 om;                                                                          \
         addr(st + MAP_SETS * stride, r, om);                                                    \
+        stamp(0);                                                                               \
         if (WCG_NOWAIT) set_wait_##S(63, m##S); /* diagnostics only: results are wrong */       \
         else if (WCG_WAIT0) set_wait_##S(0, m##S);                                              \
         else set_wait_##S((MAP_SETS - 1) + h1 + (MAP_SETS == 4 ? h2 + h3 : 0), m##S);           \
+        stamp(1);                                                                               \
         const u32 it_ = process(st, u4(m##S));                                                  \
         set_load_##S(r, om, m##S);                                                              \
         h3 = h2; h2 = h1; h1 = it_;                                                             \
@@ -929,6 +947,8 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     for (; st < nsteps; st += stride)     // tail steps: byte-exact reloads
         process(st, load_chunk(a.in, a.n, (long)(st * MAP_STEP) - 16 + 16 * lane));
 
+    if (WCG_STAMPS && lane == 0)
+        for (int i = 0; i < MAP_NSTAMP; i++) atomicAdd((unsigned long long*)&a.stamps[i], (unsigned long long)stp[i]);
     // ---- flush the LDS table into this workgroup's miss-log regions (entries with counts);
     //      a full region -> global table
     __syncthreads();

@@ -25,7 +25,9 @@ EXPORTED = [
     "wcg_export", "wcg_import", "wcg_timings", "wcg_enable_timing", "wcg_stats", "wcg_ihash",
     "wcg_version", "wcg_map_file", "wcg_partition_all", "wcg_map_json", "wcg_export_count",
     "wcg_export_write", "wcg_merge_runs", "wcg_result_copy_device", "wcg_sync", "wcg_free",
+    "wcg_comm_id", "wcg_comm_init", "wcg_exchange", "wcg_gather_merge",
 ]
+COMM_ID_BYTES = 128
 
 
 class WcgError(RuntimeError):
@@ -73,6 +75,10 @@ def load() -> ctypes.CDLL:
         "wcg_result_copy_device": (I, [P, P]),
         "wcg_sync": (I, [P]),
         "wcg_free": (I, [P, P]),
+        "wcg_comm_id": (I, [P]),
+        "wcg_comm_init": (I, [P, P, I, I]),
+        "wcg_exchange": (I, [P, U32, PU64, PU64]),
+        "wcg_gather_merge": (I, [P, I, PU64, PU64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -265,6 +271,36 @@ class Engine:
                                            ctypes.byref(nk), ctypes.byref(nb)))
         return nk.value, nb.value
 
+    # -- the shuffle and the final Merge over RCCL, inside the library
+    @staticmethod
+    def comm_id() -> bytes:
+        """ncclGetUniqueId (made once, on rank 0, and handed to every rank by the host)."""
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        rc = load().wcg_comm_id(buf)
+        if rc != WCG_OK:
+            raise WcgError(rc, "wcg_comm_id: ncclGetUniqueId failed")
+        return buf.raw
+
+    def comm_init(self, comm_id: bytes, rank: int, world: int) -> None:
+        """ncclCommInitRank for this engine (collective: every rank calls it)."""
+        if len(comm_id) != COMM_ID_BYTES:
+            raise WcgError(WCG_EINVAL, "comm_init: the id is 128 bytes")
+        self._chk(self._lib.wcg_comm_init(self._ctx, comm_id, rank, world))
+
+    def exchange(self, nreduce: int) -> Tuple[int, int]:
+        """The ihash % nreduce shuffle (collective): afterwards this engine holds exactly the keys
+        of the partitions its rank owns.  Returns (units sent, units received)."""
+        snt, rcv = ctypes.c_uint64(), ctypes.c_uint64()
+        self._chk(self._lib.wcg_exchange(self._ctx, nreduce, ctypes.byref(snt), ctypes.byref(rcv)))
+        return snt.value, rcv.value
+
+    def gather_merge(self, root: int = 0) -> Tuple[int, int]:
+        """Merge of every rank's sorted run at root (collective, after reduce()); (keys, bytes) of
+        the merged file on root, (0, 0) elsewhere."""
+        nk, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        self._chk(self._lib.wcg_gather_merge(self._ctx, root, ctypes.byref(nk), ctypes.byref(nb)))
+        return nk.value, nb.value
+
     # -- host copies of the record units (the file-based shuffle of the config-5 workers)
     def export_host(self, nreduce: int, nranks: int) -> Tuple[bytes, List[int]]:
         """export() copied to host memory: (record units, units per rank)."""
@@ -293,13 +329,13 @@ class Engine:
             hip.hipFree(dev)
 
     # -- diagnostics
-    PHASES = ("map", "agg", "compact", "sort", "format")
+    PHASES = ("map", "agg", "compact", "sort", "format", "export", "exchange", "import", "gather", "merge")
 
     def timings(self) -> Tuple[dict, int]:
         """Device ms per phase of the last job (needs enable_timing) and map launch count."""
-        ms = (ctypes.c_double * 5)()
+        ms = (ctypes.c_double * 10)()
         nl = ctypes.c_uint64()
-        self._chk(self._lib.wcg_timings(self._ctx, ms, 5, ctypes.byref(nl)))
+        self._chk(self._lib.wcg_timings(self._ctx, ms, 10, ctypes.byref(nl)))
         return dict(zip(self.PHASES, list(ms))), nl.value
 
     def stats(self) -> dict:

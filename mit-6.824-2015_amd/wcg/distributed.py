@@ -90,11 +90,29 @@ def _exchange(send: torch.Tensor, send_units: List[int], group=None, unit: int =
     return recv, recv_units
 
 
+def init_comm(engine, group=None) -> None:
+    """Give the library its own RCCL communicator (wcg_comm_init): rank 0 makes the unique id,
+    torch.distributed hands it to every rank (the reference's config-5 master would carry it in
+    its RPC).  After this, shuffle() and gather_merge() run inside libwcg (wcg_exchange,
+    wcg_gather_merge) instead of through torch collectives."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    e = engine.e if isinstance(engine, TorchEngine) else engine
+    obj = [e.comm_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    e.comm_init(obj[0], rank, world)
+    if isinstance(engine, TorchEngine):
+        engine.in_library = True
+
+
 def shuffle(engine, nreduce: int, group=None) -> None:
     """The ihash shuffle: export the local aggregate by owner straight into the send buffer,
     all-to-all it, and import what this rank owns.  Afterwards `engine` holds exactly the
     (aggregated) keys of the partitions this rank owns (mapreduce.go:214-223 partitioning,
-    :242-263 gathering)."""
+    :242-263 gathering).  With init_comm() done this is one wcg_exchange call (RCCL inside the
+    library, one host read of the unit counts)."""
+    if getattr(engine, "in_library", False):
+        engine.e.exchange(nreduce)
+        return
     world = dist.get_world_size(group)
     send, units = engine.export_tensor(nreduce, world)
     recv, rcv_units = _exchange(send, units, group)
@@ -116,6 +134,11 @@ def gather_merge(engine, root: int = 0, group=None, fetch: bool = True) -> Optio
     `root`, which merges the runs on its GPU (wcg_merge_runs: ceil(log2 world) merge passes, no
     re-sort).  Returns the merged file bytes on root (fetch=False: leaves them in the root
     engine's device buffer and returns b""), None elsewhere."""
+    if getattr(engine, "in_library", False):         # wcg_gather_merge: RCCL inside the library
+        engine.e.gather_merge(root)
+        if dist.get_rank(group) != root:
+            return None
+        return engine.result() if fetch else b""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     send, nbytes = engine.result_tensor()
@@ -141,6 +164,7 @@ class TorchEngine:
     def __init__(self, engine, stream_ptr: Optional[int] = None, host_staging: bool = False):
         self.e = engine
         self.host_staging = host_staging
+        self.in_library = False                   # init_comm(): wcg_exchange / wcg_gather_merge
         cur = torch.cuda.current_stream().cuda_stream
         if stream_ptr is None:
             stream_ptr = cur

@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 import queue
 import socket
 import threading
@@ -162,6 +163,25 @@ def merge(workdir: str, fname: str, nreduce: int) -> bytes:
 # ---------------------------------------------------------------- GPU DoMap / DoReduce
 EFULL = 4                              # WCG_EFULL (include/wcg.h): aggregation table full
 
+# Quirk P2: DoMap reads its split with ONE file.Read of the split's size
+# (mapreduce.go:205-207), and Go's os.File.Read on Linux moves at most 1 GiB per call
+# (internal/poll maxRW; Go 1.16-1.20, the versions whose unicode tables are Unicode 13 like ours),
+# returning a nil error for the short read.  A split over 1 GiB is therefore mapped as its first
+# 1 GiB followed by zero bytes - the tokens of the first 1 GiB alone, since NUL separates.  The
+# GPU DoMap emulates exactly that (oracle/wc_ref.py domap_read restates it).
+READ_CAP = 1 << 30
+
+
+def read_split(path: str) -> bytes:
+    """The bytes DoMap's single Read of a split file returns (P2: at most READ_CAP)."""
+    size = os.path.getsize(path)
+    with open(path, "rb") as f:
+        b = f.read(READ_CAP)
+    if size > READ_CAP:
+        print(f"P2: split {os.path.basename(path)} is {size} bytes; DoMap's single Read maps its first "
+              f"{READ_CAP} (the reference's behaviour, emulated)", file=sys.stderr, flush=True)
+    return b
+
 
 def _sized_job(engine, nbytes: int, job):
     """Run job() on an engine sized for nbytes of input when the engine can be re-sized
@@ -189,8 +209,7 @@ def do_map(engine, job: int, workdir: str, fname: str, nreduce: int, json_interm
     name = map_name(fname, job)
     path = os.path.join(workdir, name)
     print(f"DoMap: read split {name} {os.path.getsize(path)}", flush=True)
-    with open(path, "rb") as f:
-        b = f.read()
+    b = read_split(path)
     if json_intermediates:
         parts = _sized_job(engine, len(b), lambda: engine.map_json(b, nreduce))
         for r in range(nreduce):
@@ -218,13 +237,15 @@ def do_reduce(engine, job: int, workdir: str, fname: str, nmap: int) -> None:
         print(f"DoReduce: read {name}", flush=True)
         with open(os.path.join(workdir, name), "rb") as f:
             files.append(f.read())
-    json_in = any(f[:1] == b"{" for f in files)
+    # each file by its own format: a GPU DoMap's record units, or the reference's JSON lines (a
+    # CPU DoMap, or a GPU worker with json_intermediates) - workers of one job may differ.  A record
+    # unit never starts with '{' (its first byte is a key byte or zero padding; '{' is no letter).
+    is_json = [f[:1] == b"{" for f in files]
 
     def run():
         engine.reset()
-        for data in files:
-            if json_in:
-                # the reference's -m-r JSON lines (a CPU or json_intermediates DoMap wrote them):
+        for data, js in zip(files, is_json):
+            if js:
                 # decode on the host as DoReduce's json.Decoder does (mapreduce.go:249-261), one
                 # key per line, and count the keys on the GPU
                 keys = _json_keys(data)
@@ -235,7 +256,7 @@ def do_reduce(engine, job: int, workdir: str, fname: str, nmap: int) -> None:
         engine.reduce()
         return engine.partition(1, 0)
     # one distinct key per record unit (or per JSON line) at most
-    nunits = sum(len(f) // 32 if not json_in else f.count(b"\n") for f in files)
+    nunits = sum(f.count(b"\n") if js else len(f) // 32 for f, js in zip(files, is_json))
     _atomic_write(os.path.join(workdir, merge_name(fname, job)), _sized_job(engine, 16 * nunits, run))
 
 
@@ -439,8 +460,7 @@ def run_single(nmap: int, nreduce: int, path: str, engine, workdir: str) -> byte
     for m in range(nmap):       # fewer split files than nMap (P3): open fails, as DoMap's does
         name = map_name(fname, m)
         print(f"DoMap: read split {name} {os.path.getsize(os.path.join(workdir, name))}", flush=True)
-        with open(os.path.join(workdir, name), "rb") as f:
-            b = f.read()
+        b = read_split(os.path.join(workdir, name))
         if b:
             engine.map_host(b)
     engine.reduce()

@@ -196,6 +196,20 @@ def split(buf: bytes, nmap: int) -> List[bytes]:
     return [bytes(f) for f in files]
 
 
+# DoMap reads its split with ONE file.Read(b) of the split's size (mapreduce.go:205-207).  Go's
+# os.File.Read on Linux passes at most 1 GiB to read(2) per call (internal/poll/fd_unix.go maxRW,
+# Go 1.16-1.20 - the versions whose unicode tables restate Unicode 13, like this oracle's), and the
+# error of the short read is nil, so a split larger than 1 GiB is mapped as its first 1 GiB
+# followed by zero bytes; NUL is a separator, so that is exactly the token stream of the first
+# 1 GiB alone (quirk P2).  `read_cap` is a parameter so tests can exercise the rule at small sizes.
+DOMAP_READ_CAP = 1 << 30
+
+
+def domap_read(split_bytes: bytes, read_cap: int = DOMAP_READ_CAP) -> bytes:
+    """The bytes DoMap's single Read returns (P2): the first read_cap bytes of the split."""
+    return split_bytes[:read_cap]
+
+
 def map_files(split_bytes: bytes, nreduce: int) -> List[bytes]:
     """DoMap output files mrtmp.<f>-<m>-<r> (mapreduce.go:212-230): one JSON line per token."""
     outs = [bytearray() for _ in range(nreduce)]
@@ -204,7 +218,7 @@ def map_files(split_bytes: bytes, nreduce: int) -> List[bytes]:
     return [bytes(o) for o in outs]
 
 
-def run_single(buf: bytes, nmap: int, nreduce: int) -> Dict[str, object]:
+def run_single(buf: bytes, nmap: int, nreduce: int, read_cap: int = DOMAP_READ_CAP) -> Dict[str, object]:
     """RunSingle (mapreduce.go:344-356) restated in memory. Returns every artefact."""
     splits = split(buf, nmap)
     if len(splits) != nmap:
@@ -213,6 +227,7 @@ def run_single(buf: bytes, nmap: int, nreduce: int) -> Dict[str, object]:
     counts: Dict[bytes, int] = {}
     maps = []
     for s in splits:
+        s = domap_read(s, read_cap)             # P2
         maps.append(map_files(s, nreduce))
         for t in tokens(s):
             counts[t] = counts.get(t, 0) + 1

@@ -199,3 +199,65 @@ def test_run_single_gpu(tmp_path, built):
     assert merged == wc_ref.merged_output(counts)
     for r in range(3):
         assert (tmp_path / mr.merge_name(os.path.basename(path), r)).read_bytes() == wc_ref.res_file(counts, 3, r)
+
+
+def _p2_input(nbytes):
+    """Lines of letters whose tokens straddle the read cap in the middle of a word and of a
+    2-byte rune (the P2 cut lands wherever the split's byte count says)."""
+    unit = "wörd ".encode() * 700 + b"tailtoken\n"     # ~4 KiB lines: Split stays quick at 1 GiB
+    return (unit * (nbytes // len(unit) + 1))[:nbytes] + b"end\n"
+
+
+@pytest.mark.parametrize("cap", [4096, 4097, 4099, 10000])
+def test_run_single_p2_read_cap_cpu_standin(tmp_path, monkeypatch, cap):
+    """Quirk P2 (mapreduce.go:205-207): DoMap's single Read returns at most READ_CAP bytes (1 GiB
+    in Go 1.16-1.20); a larger split is mapped as its prefix.  With the cap lowered, RunSingle's
+    merged and -res-<r> files equal the oracle's restatement (wc_ref.run_single(read_cap=...)),
+    and differ from the uncapped counts - the emulation is exercised, not bypassed."""
+    from wcg import mr
+    monkeypatch.setattr(mr, "READ_CAP", cap)
+    data = _p2_input(40_000)
+    path = tmp_path / "p2.txt"
+    path.write_bytes(data)
+    merged = mr.run_single(3, 4, str(path), StandInEngine(), str(tmp_path))
+    ref = wc_ref.run_single(data, 3, 4, read_cap=cap)
+    assert merged == ref["merged"]
+    for r in range(4):
+        assert (tmp_path / mr.merge_name("p2.txt", r)).read_bytes() == ref["res"][r]
+    assert merged != wc_ref.run_single(data, 3, 4)["merged"]
+
+
+def test_do_reduce_mixed_intermediate_formats(tmp_path):
+    """Workers of one job may write different intermediate formats (record units / the
+    reference's JSON lines); DoReduce reads each file in its own format and loses nothing."""
+    from wcg import mr
+    path, data = _input(tmp_path, 60_000)
+    fname = os.path.basename(path)
+    nmap, nreduce = 4, 3
+    n = mr.split(path, nmap, str(tmp_path), fname)
+    eng = StandInEngine()
+    for m in range(n):
+        mr.do_map(eng, m, str(tmp_path), fname, nreduce, json_intermediates=(m % 2 == 0))
+    counts = _expected(data)
+    for r in range(nreduce):
+        mr.do_reduce(eng, r, str(tmp_path), fname, n)
+        assert (tmp_path / mr.merge_name(fname, r)).read_bytes() == wc_ref.res_file(counts, nreduce, r)
+
+
+@pytest.mark.gpu
+def test_run_single_p2_split_over_1gib_gpu(tmp_path, built):
+    """A real split larger than 1 GiB (nMap = 1, 1 GiB + 5 MiB): the GPU RunSingle maps exactly
+    DoMap's first 1 GiB (P2), checked against the C oracle on that prefix."""
+    import wcg
+    from wcg import mr
+    from tests import oracle_bridge as ob
+    n = (1 << 30) + (5 << 20)
+    data = _p2_input(n)
+    path = tmp_path / "big.txt"
+    path.write_bytes(data)
+    split = wc_ref.split(data, 1)
+    assert len(split) == 1 and len(split[0]) > mr.READ_CAP
+    want = ob.merged(split[0][:mr.READ_CAP], 16)
+    with wcg.Engine(0, 0, 1 << 18) as e:
+        merged = mr.run_single(1, 3, str(path), e, str(tmp_path))
+    ob.assert_same(merged, want)
