@@ -213,6 +213,22 @@ struct MapTable {
         return false;
     }
 
+    // the same for a lane that may hold no token (valid false: no count, no insert)
+    __device__ __forceinline__ bool finish_short_v(bool valid, u64 a0, u32 h, const ProbeS& p) {
+        const bool h1 = p.x1 == a0, hit = valid && (h1 || p.x2 == a0);
+        atomicAdd(&scnt[h1 ? p.s1 : p.s2], hit ? 1u : 0u);
+        if (!valid || hit || (p.x1 != 0 && p.x2 != 0) || !admit(h)) return hit;
+        if (p.x1 == 0) {
+            const u64 old = atomicCAS(&sk0[p.s1], 0ull, a0);
+            if (old == 0 || old == a0) { atomicAdd(&scnt[p.s1], 1u); return true; }
+        }
+        if (p.x2 == 0) {
+            const u64 old = atomicCAS(&sk0[p.s2], 0ull, a0);
+            if (old == 0 || old == a0) { atomicAdd(&scnt[p.s2], 1u); return true; }
+        }
+        return false;
+    }
+
     __device__ __forceinline__ bool finish(bool valid, bool med, u64 a0, u64 a1, u32 h, const Probe& p) {
         u64* K0 = med ? mk0 : sk0;
         u32* C = med ? mcnt : scnt;

@@ -47,12 +47,16 @@ constexpr int MAP_STEP = 16 * MAP_OWN;       // 992 input bytes per wave step
 constexpr int MAP_WIN = 1024;                // bytes loaded per step: [step base - 16, + 1024)
 constexpr int MAP_WREG = MAP_WIN + 8;        // staging (+8: keyread's third word at the end)
 constexpr int MAP_SST = 512;                 // max token starts per step (992 / 2 = 496)
+#ifndef WCG_DIRECT
+#define WCG_DIRECT 0                         // 1: no start list (measured slower: r03_kmap_experiments)
+#endif
 #ifndef WCG_ADMIT2
 #define WCG_ADMIT2 1                         // k_map LDS tables admit keys on their second miss
 #endif
-constexpr int MAP_NS = WCG_ADMIT2 ? 8432 : 8624;   // LDS short-key slots (12 B each; the 2 KiB
-                                                  // admission filter takes 192 of them, the
-                                                  // LDS letter table 4.3 KiB)
+// LDS short-key slots (12 B each; the 2 KiB admission filter takes 192 of them, the LDS letter
+// table 4.3 KiB); without the start list the window staging (16 x 1032 B) and the lists
+// (16 x 1 KiB) are free for 2736 more
+constexpr int MAP_NS = (WCG_ADMIT2 ? 8432 : 8624) + (WCG_DIRECT ? 2736 : 0);
 constexpr int MAP_NM = 1024;                 // LDS medium-key slots (20 B each)
 #ifndef WCG_MAP_SETS
 #define WCG_MAP_SETS 4
@@ -538,8 +542,10 @@ constexpr u32 OOB = 0xFFFFFFF0u;
 //   tokens only counted, 7 = full but long tokens only measured and hashed
 template <int ABL>
 __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
+#if !WCG_DIRECT
     __shared__ __align__(16) uint8_t wbytes[MAP_WAVES][MAP_WREG];
     __shared__ __align__(16) uint16_t wstart[MAP_WAVES][MAP_SST];
+#endif
     __shared__ uint16_t wmask[MAP_WAVES][64];   // chunk letter masks of the wave's window
     __shared__ __align__(16) u64 sk0[MAP_NS];
     __shared__ __align__(16) u64 mk0[MAP_NM];
@@ -563,8 +569,10 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     __syncthreads();
     const LdsLetters lt{lt_idx, lt_bits};
 
+#if !WCG_DIRECT
     uint8_t* const bytes = wbytes[wave];
     uint16_t* const sst = wstart[wave];
+#endif
     u64 stp[MAP_NSTAMP] = {};                     // WCG_STAMPS: cycles per phase (wave-uniform)
     u64 t_last = WCG_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     auto stamp = [&](int i) {
@@ -576,7 +584,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     const u64 nsteps = a.ntiles;
     const u64 stride = (u64)gridDim.x * MAP_WAVES;
     // window chunk c <-> input bytes [step base - 16 + 16c, +16); lane c holds chunk c
-    u64 my_tokens = 0;                           // wave-uniform
+    u64 my_tokens = 0;                           // wave-uniform (WCG_DIRECT: per lane)
     u32 my_hits = 0, my_global = 0, my_long = 0;
 
     // miss-log stores of this workgroup: one buffer resource over its regions
@@ -598,6 +606,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         om = live ? 16 * lane + rel - 16 : OOB;                  // step 0, lane 0: wraps to OOB
     };
 
+#if !WCG_DIRECT
     // ---- token decoding.  An entry of the start list -> the key's 16 bytes from three aligned
     //      8-byte LDS reads (unaligned 8-byte LDS reads cost ~20x the LDS cycles), then the key
     //      identity of fact F4 with byte masks, and its LDS hash
@@ -871,6 +880,196 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         return (ABL == 0 || ABL >= 6) ? nsh + 2 * (iters + 1) + extra_stores : 0u;
     };
 
+#else
+    // ---- one step without a start list.  Every owner lane counts the tokens that start in its
+    //      own 16-byte chunk, one token per lane per iteration: the short keys (<= 7 bytes, the
+    //      k0 word alone) in a first pass, the others in a second.  A token of <= 15 bytes lies in
+    //      the lane's chunk and the next one, so its key bytes come from registers (the next
+    //      chunk's four dwords by DPP): no staging of the window in LDS, no compacted start list
+    //      and no key reads from LDS - a step's only LDS traffic is the table.  Within a pass the
+    //      next token's key is extracted and its probe issued before this token's probe is
+    //      finished, so two probes are in flight per lane.  A pass runs as many iterations as
+    //      the lane with the most such starts has (C2: 4.2 per step for all starts).
+    struct TokS { u64 k; u32 h; };
+    struct TokG { u64 k0, k1; u32 h; bool lng; };
+    auto process = [&](u64 step, const uint4 mine) -> u32 {
+        const long wbase = (long)(step * MAP_STEP) - 16;        // input offset of window byte 0
+        // the next chunk's dwords by DPP wave_shl:1 (all lanes active; lane 63 gets zeros)
+        const u32 D0 = mine.x, D1 = mine.y, D2 = mine.z, D3 = mine.w;
+        const u32 D4 = (u32)__builtin_amdgcn_update_dpp(0, (int)mine.x, 0x130, 0xF, 0xF, false);
+        const u32 D5 = (u32)__builtin_amdgcn_update_dpp(0, (int)mine.y, 0x130, 0xF, 0xF, false);
+        const u32 D6 = (u32)__builtin_amdgcn_update_dpp(0, (int)mine.z, 0x130, 0xF, 0xF, false);
+        const u32 D7 = (u32)__builtin_amdgcn_update_dpp(0, (int)mine.w, 0x130, 0xF, 0xF, false);
+        // ---- letter mask of the lane's chunk (as the list path: SWAR on ASCII, Go UTF-8 decode
+        //      + letter table otherwise; lane 63's last 3 bits forced to letters on that path)
+        u32 m;
+        if (all_ascii(mine)) {
+            m = ascii_mask16(mine);
+        } else {
+            m = utf8_mask_lds(mine, D4, lt);
+            if (lane == 63) m |= 0xE000u;
+        }
+        m = (m | ((u32)__builtin_amdgcn_update_dpp(0, (int)(m >> 16), 0x138, 0xF, 0xF, false) & 7u)) & 0xFFFFu;
+        wmask[wave][lane] = (uint16_t)m;                      // read by long tokens only
+        const u32 prevm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x138, 0xF, 0xF, false);   // wave_shr:1
+        const u32 nextm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x130, 0xF, 0xF, false);   // wave_shl:1
+        const bool owner = lane >= 1 && lane <= MAP_OWN;
+        const u32 starts = owner ? (m & ~((m << 1) | (prevm >> 15)) & 0xFFFFu) : 0u;
+        const u32 w32 = m | (nextm << 16);
+        u32 r8 = w32 & (w32 >> 1);                            // bit b: bytes b..b+7 all letters
+        r8 &= r8 >> 2;
+        r8 &= r8 >> 4;
+        u32 ss = starts & ~r8, so = starts & r8;
+        my_tokens += (u32)__popc(starts);
+        wave_lds_sync();                                      // wmask before the long tokens' reads
+        // the first set start of msk (false: none left), removed from msk
+        auto next_start = [](u32& msk, u32& b) -> bool {
+            const bool v = msk != 0;
+            b = v ? (u32)__builtin_ctz(msk) : 0u;
+            msk &= msk - 1;
+            return v;
+        };
+        // window dwords e_k = D[d + k], d = b >> 2 (two levels of selects)
+        auto sel = [&](u32 b, u32 (&e)[5], int n) {
+            const bool s0 = (b & 4u) != 0, s1 = (b & 8u) != 0;
+            const u32 P0 = s0 ? D1 : D0, P1 = s0 ? D2 : D1, P2 = s0 ? D3 : D2, P3 = s0 ? D4 : D3;
+            const u32 P4 = s0 ? D5 : D4;
+            e[0] = s1 ? P2 : P0; e[1] = s1 ? P3 : P1; e[2] = s1 ? P4 : P2;
+            if (n > 3) {
+                const u32 P5 = s0 ? D6 : D5, P6 = s0 ? D7 : D6;
+                e[3] = s1 ? P5 : P3; e[4] = s1 ? P6 : P4;
+            }
+        };
+        auto short_at = [&](u32 b) -> TokS {
+            const u32 len = (u32)__builtin_ctz(~(w32 >> b));   // 1..7 for a short start
+            u32 e[5];
+            sel(b, e, 3);
+            const u32 bs = b & 3u;
+            const u64 w = (u64)__builtin_amdgcn_alignbyte(e[2], e[1], bs) << 32 | __builtin_amdgcn_alignbyte(e[1], e[0], bs);
+            TokS t;
+            t.k = (w & ((1ull << (8 * len)) - 1)) | (u64)len << 56;
+            t.h = lds_hash32((u32)t.k, (u32)(t.k >> 32), 0u, 0u);
+            return t;
+        };
+        auto gen_at = [&](u32 b) -> TokG {
+            const u32 run = (u32)__builtin_ctz(~(w32 >> b));   // >= 8; 32 - b if all letters
+            const u32 len = run < 16 ? run : 16u;              // 16 = long token (> 15 bytes)
+            u32 e[5];
+            sel(b, e, 5);
+            const u32 bs = b & 3u;
+            const u32 w0 = __builtin_amdgcn_alignbyte(e[1], e[0], bs), w1 = __builtin_amdgcn_alignbyte(e[2], e[1], bs);
+            const u32 w2 = __builtin_amdgcn_alignbyte(e[3], e[2], bs), w3 = __builtin_amdgcn_alignbyte(e[4], e[3], bs);
+            const u32 nb = len - 8;                            // bytes in k1: 0..7 (8 for a long token)
+            const u32 ml = nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1;
+            const u32 mh = nb >= 8 ? 0xFFFFFFFFu : (nb >= 4 ? (1u << (8 * nb - 32)) - 1 : 0u);
+            TokG t;
+            t.k0 = (u64)w1 << 32 | w0;
+            t.k1 = (u64)((w3 & mh) | (len << 24)) << 32 | (w2 & ml);
+            t.lng = len >= 16;
+            t.h = lds_hash32(w0, w1, (u32)t.k1, (u32)(t.k1 >> 32));
+            return t;
+        };
+
+        // miss-log units: a miss reserves its units with an LDS atomic whose result is read one
+        // iteration later, and the wave stores them then (1 store per short iteration, 2 per
+        // other iteration, 2 at the end: the prefetch accounting)
+        bool missp = false;
+        u32 pp = 0, nup = 0, posp = 0;
+        u64 k0p = 0, k1p = 0;
+        const u32 rcap = (u32)a.region_cap;   // < 2^22 (host), so offsets fit 24-bit multiplies
+        auto store_pending = [&](bool two) {
+            const bool fits = missp && posp + nup <= rcap;
+            const u32 o0 = fits ? (__umul24(pp, rcap) + posp) * 8u : OOB;
+            unit_store(prsrc, o0, k0p);
+            if (two) unit_store(prsrc, fits && nup == 2 ? o0 + 8u : OOB, k1p);
+            if (missp && !fits) {             // region full: zero its tail, global table
+                u64* r = wpool + (u64)pp * a.region_cap;
+                for (u32 k = posp; k < rcap; k++) r[k] = 0;
+                my_global++;
+                ginsert(a.gtab, a.gmask, k0p, k1p, gslot(key_hash(k0p, k1p)), 1, a.st);
+            }
+        };
+        u32 n_s = 0, n_o = 0;
+        // Each pass is unrolled by two with fixed roles (token A, token B): a loop-carried copy of
+        // a probe's result registers would wait for its reads (lgkmcnt) before the next probe
+        // is issued, which is exactly the overlap the pipeline is for.
+        // ---- short keys
+        {
+            auto finish_s = [&](bool v, const TokS& t, const typename decltype(tab)::ProbeS& pr) {
+                const bool hit = tab.finish_short_v(v, t.k, t.h, pr);
+                my_hits += (u32)hit;
+                store_pending(false);
+                missp = v && !hit;
+                pp = miss_bucket(t.h, a.pmask);
+                nup = 1u;
+                posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
+                k0p = t.k; k1p = 0;
+                n_s++;
+            };
+            u32 bA, bB;
+            bool vA = next_start(ss, bA), vB;
+            TokS A = short_at(bA), B;
+            auto prA = tab.probe_short(A.h);
+            decltype(prA) prB;
+            while (__ballot(vA)) {
+                vB = next_start(ss, bB);
+                B = short_at(bB);
+                prB = tab.probe_short(B.h);
+                __builtin_amdgcn_sched_barrier(0);            // B's probe reads issue before A's wait
+                finish_s(vA, A, prA);
+                if (!__ballot(vB)) break;
+                vA = next_start(ss, bA);
+                A = short_at(bA);
+                prA = tab.probe_short(A.h);
+                __builtin_amdgcn_sched_barrier(0);
+                finish_s(vB, B, prB);
+            }
+        }
+        // ---- medium (8-15 bytes) and long keys
+        {
+            auto finish_g = [&](bool v, u32 b, const TokG& t, const typename decltype(tab)::Probe& pr) {
+                if (v && t.lng) {
+                    my_long++;
+                    const u32 rp = 16 * lane + b;
+                    long_token_log<ABL>(a, (u64)(wbase + rp), rp, wmask[wave], &lcur);
+                }
+                const bool val = v && !t.lng;
+                const bool hit = tab.finish(val, true, t.k0, t.k1, t.h, pr);
+                my_hits += (u32)hit;
+                store_pending(true);
+                missp = val && !hit;
+                pp = miss_bucket(t.h, a.pmask);
+                nup = 2u;
+                posp = atomicAdd(&cursor[pp], missp ? 2u : 0u);
+                k0p = t.k0; k1p = t.k1;
+                n_o++;
+            };
+            u32 bA, bB;
+            bool vA = next_start(so, bA), vB;
+            TokG A = gen_at(bA), B;
+            auto prA = tab.probe(true, A.h);
+            decltype(prA) prB;
+            while (__ballot(vA)) {
+                vB = next_start(so, bB);
+                B = gen_at(bB);
+                prB = tab.probe(true, B.h);
+                __builtin_amdgcn_sched_barrier(0);
+                finish_g(vA, bA, A, prA);
+                if (!__ballot(vB)) break;
+                vA = next_start(so, bA);
+                A = gen_at(bA);
+                prA = tab.probe(true, A.h);
+                __builtin_amdgcn_sched_barrier(0);
+                finish_g(vB, bB, B, prB);
+            }
+        }
+        store_pending(true);
+        wave_lds_sync();
+        if (WCG_STAMPS) stp[6]++;
+        return n_s + 2 * n_o + 2;
+    };
+#endif
+
     // ---- main loop, unrolled over the register sets so that each set's load and waits name
     //      fixed registers (tools/check_inflight.py); a set's load was issued MAP_SETS steps
     //      earlier; h1..h3 = unit stores of the last three steps (the wait count)
@@ -971,7 +1170,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     // to DevState).  Per-wave atomics on DevState cost ~12 ns each serialised on one line:
     // 16K of them added 0.2 ms to every launch.
     __shared__ u64 wsum[MAP_WAVES][4];
-    u64 v0 = lane == 0 ? my_tokens : 0, v1 = my_hits, v2 = my_global, v3 = my_long;
+    u64 v0 = (WCG_DIRECT || lane == 0) ? my_tokens : 0, v1 = my_hits, v2 = my_global, v3 = my_long;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         v0 += __shfl_xor(v0, d, 64); v1 += __shfl_xor(v1, d, 64);
