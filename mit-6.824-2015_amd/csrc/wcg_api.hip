@@ -844,17 +844,10 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     a.n = n;
     a.ntiles = (n + MAP_STEP - 1) / MAP_STEP;      // 992-byte wave steps (1 KiB windows)
     // one workgroup per CU (LDS-bound); steps are dealt chip-wide inside the kernel
-    u64 grid = std::min<u64>((u64)c->ncu, (a.ntiles + MAP_WAVES - 1) / MAP_WAVES);
+    u64 grid = std::min<u64>((u64)c->ncu * MAP_WGS, (a.ntiles + MAP_WAVES - 1) / MAP_WAVES);
     // steps per workgroup (sizing only): wave w of workgroup g takes steps g*16 + w + k*G*16, so
     // a workgroup runs at most MAP_WAVES * ceil(ntiles / (G * MAP_WAVES)) of them
     a.tiles_per_wg = MAP_WAVES * ((a.ntiles + grid * MAP_WAVES - 1) / (grid * MAP_WAVES));
-    {   // WCG_EVICT builds: refresh the LDS table after an eighth of every wave's steps (a wave runs at
-        // least floor(ntiles / (grid * 16)) steps; the last two may be tail steps)
-        const u64 minsteps = a.ntiles / (grid * MAP_WAVES);
-        static const char* em = getenv("WCG_EVICT_MIN");
-        a.evict_min = em ? (u32)atoi(em) : 2;
-        a.evict_at = minsteps >= 64 ? (u32)(minsteps / 8) : 0;
-    }
     a.gtab = c->gtab; a.gmask = c->gslots - 1;
     a.ltab = c->ltab; a.lmask = c->lslots - 1;
     a.arena = c->arena; a.arena_cap = c->arena_cap;

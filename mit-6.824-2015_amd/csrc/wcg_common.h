@@ -144,8 +144,17 @@ __device__ __forceinline__ u32 ascii_mask4(u32 x) {
     u32 hi = a & ~b & 0x80808080u;
     return (((hi >> 7) * 0x00204081u) >> 21) & 0xFu;
 }
+// 16 ASCII bytes -> letter mask.  The letter flags sit in bit 7 of each byte; one multiply by
+// 2^0 + 2^7 + 2^14 + 2^21 gathers the four flags of a dword into bits 28-31 (the partial
+// products land on distinct bits: no carries), and each nibble is shifted straight to its place
+__device__ __forceinline__ u32 ascii_hi4(u32 x) {
+    const u32 t = x | 0x20202020u;
+    return (t + 0x1F1F1F1Fu) & ~(t + 0x05050505u) & 0x80808080u;   // >= 'a' and < '{'
+}
 __device__ __forceinline__ u32 ascii_mask16(uint4 v) {
-    return ascii_mask4(v.x) | (ascii_mask4(v.y) << 4) | (ascii_mask4(v.z) << 8) | (ascii_mask4(v.w) << 12);
+    constexpr u32 G = 0x00204081u;
+    return ((ascii_hi4(v.x) * G) >> 28) | (((ascii_hi4(v.y) * G) >> 24) & 0xF0u) |
+           (((ascii_hi4(v.z) * G) >> 20) & 0xF00u) | (((ascii_hi4(v.w) * G) >> 16) & 0xF000u);
 }
 __device__ __forceinline__ bool all_ascii(uint4 v) { return ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0; }
 

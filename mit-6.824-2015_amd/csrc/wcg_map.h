@@ -40,7 +40,14 @@
 
 namespace wcg {
 
-constexpr int MAP_NT = 1024;                 // threads per workgroup
+#ifndef WCG_MAP_NT
+#define WCG_MAP_NT 1024
+#endif
+#ifndef WCG_MAP_WGS
+#define WCG_MAP_WGS 1                        // workgroups per CU (LDS and registers split between them)
+#endif
+constexpr int MAP_NT = WCG_MAP_NT;           // threads per workgroup
+constexpr int MAP_WGS = WCG_MAP_WGS;
 constexpr int MAP_WAVES = MAP_NT / 64;       // 16 independent waves
 constexpr int MAP_OWN = 62;                  // chunks owned per step (lanes 1-62)
 constexpr int MAP_STEP = 16 * MAP_OWN;       // 992 input bytes per wave step
@@ -56,21 +63,18 @@ constexpr int MAP_SST = 512;                 // max token starts per step (992 /
 // LDS short-key slots (12 B each; the 2 KiB admission filter takes 192 of them, the LDS letter
 // table 4.3 KiB); without the start list the window staging (16 x 1032 B) and the lists
 // (16 x 1 KiB) are free for 2736 more
-constexpr int MAP_NS = (WCG_ADMIT2 ? 8432 : 8624) + (WCG_DIRECT ? 2736 : 0);
-constexpr int MAP_NM = 1024;                 // LDS medium-key slots (20 B each)
+#ifndef WCG_MAP_NS
+#define WCG_MAP_NS ((WCG_ADMIT2 ? 8432 : 8624) + (WCG_DIRECT ? 2736 : 0))
+#endif
+#ifndef WCG_MAP_NM
+#define WCG_MAP_NM 1024
+#endif
+constexpr int MAP_NS = WCG_MAP_NS;
+constexpr int MAP_NM = WCG_MAP_NM;           // LDS medium-key slots (20 B each)
 #ifndef WCG_MAP_SETS
 #define WCG_MAP_SETS 4
 #endif
 constexpr int MAP_SETS = WCG_MAP_SETS;       // steps in flight per wave (2 or 4)
-#ifndef WCG_SHORT_PAIR
-#define WCG_SHORT_PAIR 0                     // 1: short-key iterations in pairs (two tokens per lane)
-#endif
-#ifndef WCG_MASKED_RESERVE
-#define WCG_MASKED_RESERVE 0                 // 1: miss reservations by the missing lanes only
-#endif
-#ifndef WCG_EVICT
-#define WCG_EVICT 0                          // 1: one refresh of the LDS table part-way (evict_at)
-#endif
 #ifndef WCG_WAIT0
 #define WCG_WAIT0 0                          // diagnostics: 1 = wait for every older memory op
 #endif
@@ -101,8 +105,6 @@ struct MapArgs {
     u64* llog;     u32 llog_cap;    // long-token log: region wg = llog[wg * llog_cap ...]
     u32* llog_len;                 // records written per region
     Rec* emit;     u64 emit_cap;    // two-pass jobs: the record log (k_long_hash's inline runs)
-    u32 evict_at;                   // WCG_EVICT: after this many steps per wave, the LDS table
-    u32 evict_min;                  //   drops entries counted fewer than evict_min times (0: never)
     u64* stamps;                    // WCG_STAMPS builds: MAP_NSTAMP sums over all waves
 };
 constexpr u64 LLOG_OFF_MASK = (1ull << 40) - 1;   // record = input offset | len << 40 (len 0: walk)
@@ -536,12 +538,25 @@ __device__ __forceinline__ void unit_store(v4i rsrc, u32 off, u64 v) {
 }
 constexpr u32 OOB = 0xFFFFFFF0u;
 
+// inclusive prefix sum over the 64 lanes by DPP: within rows (row_shr 1-3 of the input, then
+// row_shr 4 / 8 on banks 1-3 / 2-3), then across rows (row_bcast 15 / 31)
+__device__ __forceinline__ u32 wave_incl_scan(u32 x) {
+    u32 s = x + (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true)
+              + (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true)
+              + (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x113, 0xF, 0xF, true);
+    s += (u32)__builtin_amdgcn_update_dpp(0, (int)s, 0x114, 0xF, 0xE, true);
+    s += (u32)__builtin_amdgcn_update_dpp(0, (int)s, 0x118, 0xF, 0xC, true);
+    s += (u32)__builtin_amdgcn_update_dpp(0, (int)s, 0x142, 0xA, 0xF, false);
+    s += (u32)__builtin_amdgcn_update_dpp(0, (int)s, 0x143, 0xC, 0xF, false);
+    return s;
+}
+
 // ABL (measurement builds only, selected by WCG_MAP_ABLATE; results are wrong when ABL != 0):
 //   5 = input loads only, 4 = + LDS staging and letter masks, 1 = + token starts and compaction,
 //   2 = + key extraction and hash, 3 = + LDS lookup with misses dropped; 6 = full but long
 //   tokens only counted, 7 = full but long tokens only measured and hashed
 template <int ABL>
-__global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
+__global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs a) {
 #if !WCG_DIRECT
     __shared__ __align__(16) uint8_t wbytes[MAP_WAVES][MAP_WREG];
     __shared__ __align__(16) uint16_t wstart[MAP_WAVES][MAP_SST];
@@ -585,6 +600,8 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
     const u64 stride = (u64)gridDim.x * MAP_WAVES;
     // window chunk c <-> input bytes [step base - 16 + 16c, +16); lane c holds chunk c
     u64 my_tokens = 0;                           // wave-uniform (WCG_DIRECT: per lane)
+    // token starts are owned by lanes 1-62 only (lane 0: the prefix chunk, 63: the look-ahead)
+    const u32 own16 = (u32)(lane - 1) < (u32)MAP_OWN ? 0xFFFFu : 0u;
     u32 my_hits = 0, my_global = 0, my_long = 0;
 
     // miss-log stores of this workgroup: one buffer resource over its regions
@@ -668,8 +685,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         // neighbours' masks by DPP lane shifts
         const u32 prevm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x138, 0xF, 0xF, false);   // wave_shr:1
         const u32 nextm = (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0x130, 0xF, 0xF, false);   // wave_shl:1
-        const bool owner = lane >= 1 && lane <= MAP_OWN;
-        u32 starts = owner ? (m & ~((m << 1) | (prevm >> 15)) & 0xFFFFu) : 0u;
+        u32 starts = m & ~((m << 1) | (prevm >> 15)) & own16;
         const u32 w32 = m | (nextm << 16);
         // Start list, short keys (<= 7 bytes: 89% of C2 tokens) first, then the others: a start
         // whose letter run reaches 8 bytes has bits b..b+7 of w32 set.  Iterations over short
@@ -677,26 +693,26 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         u32 r8 = w32 & (w32 >> 1);
         r8 &= r8 >> 2;
         r8 &= r8 >> 4;
-        const u32 cs = __popc(starts & ~r8), co = __popc(starts & r8);
-        u32 o_s = 0, o_o = 0, tot_s = 0, tot_o = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const u64 bs = __ballot((cs >> b) & 1), bo = __ballot((co >> b) & 1);
-            o_s += __builtin_amdgcn_mbcnt_hi((u32)(bs >> 32), __builtin_amdgcn_mbcnt_lo((u32)bs, 0u)) << b;
-            o_o += __builtin_amdgcn_mbcnt_hi((u32)(bo >> 32), __builtin_amdgcn_mbcnt_lo((u32)bo, 0u)) << b;
-            tot_s += (u32)__popcll(bs) << b;
-            tot_o += (u32)__popcll(bo) << b;
-        }
-        tot_s = __builtin_amdgcn_readfirstlane(tot_s);
-        const u32 total = tot_s + __builtin_amdgcn_readfirstlane(tot_o);
-        o_o += tot_s;
+        // both counts in one word (each <= 16 per lane, <= 496 per wave) and ONE wave-wide DPP
+        // prefix sum for the lanes' list offsets (4 bit-plane ballots + mbcnt per count were ~4x
+        // the VALU)
+        const u32 packed = (u32)__popc(starts & ~r8) | (u32)__popc(starts & r8) << 16;
+        const u32 incl = wave_incl_scan(packed);
+        const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+        const u32 tot_s = tot & 0xFFFFu;
+        const u32 total = tot_s + (tot >> 16);
+        const u32 excl = incl - packed;
+        u32 o_s = excl & 0xFFFFu, o_o = (excl >> 16) + tot_s;
+        // one loop over all starts (two loops, short and other, ran max(short) + max(other) =
+        // 4.2 + 1.6 iterations per step against max(all) = 4.2)
+        const u32 lbase = 16 * lane;
         while (starts) {
             const u32 b = __builtin_ctz(starts);
             starts &= starts - 1;
             const u32 run = __builtin_ctz(~(w32 >> b));        // >= 1; 32 - b when the window is all letters
             const u32 len = run < 16 ? run : 16u;              // 16 = long token (> 15 bytes)
             const bool sh = len < 8;
-            sst[sh ? o_s : o_o] = (uint16_t)((16 * lane + b) | (len << SST_LEN_SHIFT));
+            sst[sh ? o_s : o_o] = (uint16_t)((lbase + b) | (len << SST_LEN_SHIFT));
             o_s += sh ? 1u : 0u;
             o_o += sh ? 0u : 1u;
         }
@@ -716,9 +732,6 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         bool missp = false;                   // the previous iteration's miss: bucket, units,
         u32 pp = 0, nup = 0, posp = 0;        // reservation and key
         u64 k0p = 0, k1p = 0;
-        bool missq = false;                   // paired short iterations: the second token's
-        u32 pq = 0, posq = 0;
-        u64 k0q = 0;
         const u32 rcap = (u32)a.region_cap;   // < 2^22 (host), so offsets fit 24-bit multiplies
         auto store_pending = [&](bool two) {
             const bool fits = missp && posp + nup <= rcap;
@@ -732,18 +745,6 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
                 ginsert(a.gtab, a.gmask, k0p, k1p, gslot(key_hash(k0p, k1p)), 1, a.st);
             }
         };
-        auto store_pending_q = [&]() {        // the paired loop's second pending short key
-            const bool fits = missq && posq + 1 <= rcap;
-            unit_store(prsrc, fits ? (__umul24(pq, rcap) + posq) * 8u : OOB, k0q);
-            if (missq && !fits) {
-                u64* r = wpool + (u64)pq * a.region_cap;
-                for (u32 k = posq; k < rcap; k++) r[k] = 0;
-                my_global++;
-                ginsert(a.gtab, a.gmask, k0q, 0, gslot(key_hash(k0q, 0)), 1, a.st);
-            }
-            missq = false;
-        };
-        u32 extra_stores = 0;
         // full iterations of short entries take the short body; the rest (the partial short
         // iteration, medium and long keys) the general one
         const u32 nsh = (ABL == 0 || ABL >= 6) ? (tot_s >> 6) : 0u;
@@ -776,40 +777,9 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
                 return t;
             };
             u32 it = 0;
-#if WCG_SHORT_PAIR
-            // pairs of full short iterations: two tokens per lane, both probes and both next
-            // keys in one LDS round trip; each token's miss is stored one pair later (1 store per
-            // token, + 1 for the second pending slot after the loop)
-            if (nsh >= 2) {
-                TokS ca = decode_s(sst[lane], keyread_s(sst[lane]));
-                TokS cb = decode_s(sst[64 + lane], keyread_s(sst[64 + lane]));
-                u32 ea = sst[128 + lane], eb = sst[192 + lane];
-                for (; it + 2 <= nsh; it += 2) {
-                    const auto pa = tab.probe_short(ca.h);
-                    const auto pb = tab.probe_short(cb.h);
-                    const uint4 na = keyread_s(ea), nb = keyread_s(eb);
-                    const u32 ean = sst[(it + 4) * 64 + lane], ebn = sst[(it + 5) * 64 + lane];
-                    __builtin_amdgcn_sched_barrier(0);
-                    const bool ha = tab.finish_short(ca.k, ca.h, pa);
-                    const bool hb = tab.finish_short(cb.k, cb.h, pb);
-                    my_hits += (u32)ha + (u32)hb;
-                    store_pending(false);
-                    store_pending_q();
-                    missp = !ha; pp = miss_bucket(ca.h, a.pmask); nup = 1u; k0p = ca.k; k1p = 0;
-                    missq = !hb; pq = miss_bucket(cb.h, a.pmask); k0q = cb.k;
-                    posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
-                    posq = atomicAdd(&cursor[pq], missq ? 1u : 0u);
-                    ca = decode_s(ea, na);
-                    cb = decode_s(eb, nb);
-                    ea = ean; eb = ebn;
-                }
-                store_pending_q();
-                extra_stores = 1;
-            }
-#endif
             TokS cs = decode_s(sst[it * 64 + lane], keyread_s(sst[it * 64 + lane]));
             e_nxt = sst[(it + 1) * 64 + lane];
-            for (; it < nsh; it++) {
+            for (; it + 1 < nsh; it++) {
                 const auto pr = tab.probe_short(cs.h);
                 const uint4 nks = keyread_s(e_nxt);
                 const u32 e_nn = sst[(it + 2) * 64 + lane];
@@ -820,24 +790,37 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
                 missp = !hit;
                 pp = miss_bucket(cs.h, a.pmask);
                 nup = 1u;
-#if WCG_MASKED_RESERVE
-                if (missp) posp = atomicAdd(&cursor[pp], 1u);   // only missing lanes touch the cursors
-#else
                 posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
-#endif
                 k0p = cs.k; k1p = 0;
                 cs = decode_s(e_nxt, nks);
                 e_nxt = e_nn;
             }
-            e_nxt = sst[first + lane];
+            // the last short iteration decodes the general loop's first token (entry first +
+            // lane, already in e_nxt) with the general decoder: no prologue round trips there
+            {
+                const auto pr = tab.probe_short(cs.h);
+                const KeyWords nkw = keyread(e_nxt);
+                const u32 e_nn = sst[(it + 2) * 64 + lane];
+                __builtin_amdgcn_sched_barrier(0);
+                const bool hit = tab.finish_short(cs.k, cs.h, pr);
+                my_hits += (u32)hit;
+                store_pending(false);
+                missp = !hit;
+                pp = miss_bucket(cs.h, a.pmask);
+                nup = 1u;
+                posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
+                k0p = cs.k; k1p = 0;
+                cur = decode_tok(e_nxt, first + lane < total, nkw);
+                e_nxt = e_nn;
+            }
         } else {
             e_nxt = sst[lane];
+            if (iters) {
+                cur = decode_tok(e_nxt, first + lane < total, keyread(e_nxt));
+                e_nxt = sst[first + 64 + lane];
+            }
         }
         stamp(4);
-        if (iters) {
-            cur = decode_tok(e_nxt, first + lane < total, keyread(e_nxt));
-            e_nxt = sst[first + 64 + lane];
-        }
         for (u32 it = 0; it < iters; it++) {
             const u32 base = first + it * 64;
             if (ABL == 1) { sink += cur.e; cur.e = sst[base + 64 + lane]; continue; }
@@ -863,11 +846,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
             missp = cur.valid && !hit;
             pp = miss_bucket(cur.h, a.pmask);
             nup = cur.shrt ? 1u : 2u;
-#if WCG_MASKED_RESERVE
-            if (missp) posp = atomicAdd(&cursor[pp], nup);
-#else
             posp = atomicAdd(&cursor[pp], missp ? nup : 0u);   // every lane (0 = no miss)
-#endif
             k0p = k0; k1p = k1;
             cur = decode_tok(e_nxt, base + 64 + lane < total, nkw);
             e_nxt = e_nn;
@@ -877,7 +856,7 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         wave_lds_sync();
         stamp(5);
         if (WCG_STAMPS) stp[6]++;
-        return (ABL == 0 || ABL >= 6) ? nsh + 2 * (iters + 1) + extra_stores : 0u;
+        return (ABL == 0 || ABL >= 6) ? nsh + 2 * (iters + 1) : 0u;
     };
 
 #else
@@ -1087,31 +1066,6 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         }
     }
     u32 h1 = 0, h2 = 0, h3 = 0;
-    // WCG_EVICT: one refresh of the table once every wave has run evict_at steps (the host picks
-    // evict_at below every wave's step count, so all 16 waves reach the barriers): entries counted
-    // fewer than evict_min times go to the miss log with their counts and free their slots (and
-    // the admission filter restarts), so keys that became frequent since can take them.  Exact:
-    // every occurrence stays counted once, in the table or in the log.
-    u32 kstep = 0;
-    auto evict = [&]() {
-        __syncthreads();
-        auto out = [&](u64 k0, u64 k1, u32 c) {
-            if (!log_push(a, cursor, miss_bucket(lds_hash(k0, k1), a.pmask), k0, k1, c)) {
-                my_global++;
-                ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
-            }
-        };
-        for (int i = tid; i < MAP_NS; i += MAP_NT) {
-            const u32 c = scnt[i];
-            if (sk0[i] != 0 && c < a.evict_min) { if (c) out(sk0[i], 0, c); sk0[i] = 0; scnt[i] = 0; }
-        }
-        for (int i = tid; i < MAP_NM; i += MAP_NT) {
-            const u32 c = mcnt[i];
-            if (mk0[i] != 0 && c < a.evict_min) { if (c) out(mk0[i], mk1[i], c); mk0[i] = 0; mk1[i] = 0; mcnt[i] = 0; }
-        }
-        if (WCG_ADMIT2) for (int i = tid; i < (int)(MapTable<MAP_NS, MAP_NM>::ADMIT_BITS / 32); i += MAP_NT) seen_w[i] = 0;
-        __syncthreads();
-    };
 #define WCG_MAP_STEP(S)                                                                         \
     {                                                                                           \
         if (st >= nsteps || is_tail(st)) break;                                                 \
@@ -1126,7 +1080,6 @@ __global__ __launch_bounds__(MAP_NT) void k_map(MapArgs a) {
         set_load_##S(r, om, m##S);                                                              \
         h3 = h2; h2 = h1; h1 = it_;                                                             \
         st += stride;                                                                           \
-        if (WCG_EVICT && ++kstep == a.evict_at) evict();                                        \
     }
     while (true) {
         WCG_MAP_STEP(A)
