@@ -834,9 +834,16 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
             if (ABL == 2) { sink += cur.h; cur = decode_tok(e_nxt, base + 64 + lane < total, keyread(e_nxt));
                             e_nxt = sst[base + 128 + lane]; continue; }
             // issue together: this token's probe, the next token's key bytes, the entry after
+            // (none of it in the last iteration: C2 steps run one general iteration, so its
+            // next-token reads and decode were pure waste, ~40 VALU per step)
+            const bool more = it + 1 < iters;
             const auto pr = tab.probe(med, cur.h);
-            const KeyWords nkw = keyread(e_nxt);
-            const u32 e_nn = sst[base + 128 + lane];
+            KeyWords nkw{};
+            u32 e_nn = 0;
+            if (more) {
+                nkw = keyread(e_nxt);
+                e_nn = sst[base + 128 + lane];
+            }
             __builtin_amdgcn_sched_barrier(0);
             const bool hit = tab.finish(cur.valid, med, k0, k1, cur.h, pr);
             if (ABL == 3) { sink += hit; cur = decode_tok(e_nxt, base + 64 + lane < total, nkw); e_nxt = e_nn; continue; }
@@ -848,8 +855,10 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
             nup = cur.shrt ? 1u : 2u;
             posp = atomicAdd(&cursor[pp], missp ? nup : 0u);   // every lane (0 = no miss)
             k0p = k0; k1p = k1;
-            cur = decode_tok(e_nxt, base + 64 + lane < total, nkw);
-            e_nxt = e_nn;
+            if (more) {
+                cur = decode_tok(e_nxt, base + 64 + lane < total, nkw);
+                e_nxt = e_nn;
+            }
         }
         if (ABL == 0 || ABL >= 6) store_pending(true);
         if (ABL) asm volatile("" ::"v"(sink));
