@@ -36,10 +36,9 @@ constexpr u32 AGG_MAX_SRC = 256;       // source regions per workgroup (+1 KiB L
 constexpr u32 AGG_Q = 128;             // pass-2 sub-buckets per bucket
 constexpr u32 AGG_OVF_CAP = 4096;      // pass 2: overflow records staged per workgroup (128 KiB)
 constexpr int AGG_SPILL = 0, AGG_EMIT = 1;
-#ifndef WCG_AGG_SETS1
-#define WCG_AGG_SETS1 2
+#ifndef WCG_AGG_ABLATE
+#define WCG_AGG_ABLATE 0       // diagnostics: 1 = loads only, 2 = + decode and hash (wrong counts)
 #endif
-constexpr int AGG_SETS1 = WCG_AGG_SETS1;   // pass 1: wave batches in flight (pass 2: 2)
 
 struct AggArgs {
     // sources: bucket b's regions are pool + ((wbase + k * wstep) * rstride + b % rmod) * region_cap
@@ -65,6 +64,7 @@ struct AggArgs {
     u64 emit_cap;
     Rec* ovf;              // pass 2: per-workgroup staging of the entries a full LDS table
     u32 ovf_cap;           //   cannot take (ovf_cap records per workgroup)
+    u64* clk;              // diagnostics (WCG_AGG_CLOCK): per workgroup start / end wall clock, or null
 };
 
 // bucket choices of pass 2's tables: the high half of the 64-bit key hash (a sub-bucket's keys
@@ -90,6 +90,24 @@ __device__ __forceinline__ void agg_decode(const u64 (&u)[6], u64 (&k0)[4], u64 
     }
 }
 
+// k_agg's prefetch register sets: three tagged 16-byte loads per set and a wait naming the set's
+// registers (tools/check_inflight.py; the k_map sets use the same tags with one load each)
+#define WCG_AGG_SET_OPS(S)                                                                      \
+    __device__ __forceinline__ void agg_load_##S(const v4u* q, v4u& x0, v4u& x1, v4u& x2) {     \
+        asm volatile("global_load_dwordx4 %0, %3, off ; wcg-load " #S "0\n\t"                   \
+                     "global_load_dwordx4 %1, %3, off offset:16 ; wcg-load " #S "1\n\t"         \
+                     "global_load_dwordx4 %2, %3, off offset:32 ; wcg-load " #S "2"              \
+                     : "=&v"(x0), "=&v"(x1), "=&v"(x2) : "v"(q) : "memory");                    \
+    }                                                                                           \
+    template <int N>                                                                            \
+    __device__ __forceinline__ void agg_wait_##S(v4u& x0, v4u& x1, v4u& x2) {                   \
+        asm volatile("s_waitcnt vmcnt(%3) ; wcg-wait " #S " %0 %1 %2"                            \
+                     : "+v"(x0), "+v"(x1), "+v"(x2) : "n"(N) : "memory");                       \
+    }
+WCG_AGG_SET_OPS(A)
+WCG_AGG_SET_OPS(B)
+#undef WCG_AGG_SET_OPS
+
 // One (bucket, slice) of k_agg: index bi = p + P * s.  Returns the global-table inserts made.
 // MODE is a template parameter: one kernel for both passes held the union of their registers
 // (128 VGPRs with a spill)
@@ -97,6 +115,9 @@ template <int MODE>
 __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[AGG_W], u64 (*tcnt)[AGG_W], u32* rlen_s,
                        u32* bstart, u32& spos, u64 (*wsum)[4]) {
     const int tid = threadIdx.x;
+    // (a first-fit variant that reads b2's row only when b1 is full - half the LDS bytes - measured
+    // slower on C2, 0.333 vs 0.310 ms: a wave waits for the second round trip whenever any of its
+    // lanes needs it)
     LdsTable<AGG_NB, u64, AGG_W> tab{tk0, tk1, tcnt};
     constexpr bool emit = MODE == AGG_EMIT;
     const u32 p = bi % a.P, s = bi / a.P;
@@ -163,7 +184,9 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
     // per CU (a workgroup-wide batch walk kept only 2, and ran at the HBM latency of one batch
     // per region even for nearly empty regions; a region per wave left most waves idle when a
     // workgroup has few regions, as in pass 2).
-    const int wave = tid >> 6, lane = tid & 63;
+    // the wave index as a scalar: the batch walk below is then uniform control flow (a per-lane
+    // `wave` made the compiler run it as a divergent loop, with its region state spilled)
+    const u32 wave = (u32)__builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     constexpr u32 WSTRIDE = AGG_NT / 64;
     // (region k, batch b) of a wave's batch g, advanced incrementally: g grows by WSTRIDE per
     // step, which crosses at most a few region ends
@@ -184,13 +207,12 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
             k++;
         }
     };
-    auto load = [&](u32 k, u32 b, v4u& x0, v4u& x1, v4u& x2) {
+    // a batch's units: lane l reads [4l, 4l + 6) of the batch (a dead batch, k >= nk, reads the
+    // first batch of the first region: the loads are unconditional, see below)
+    auto batch_ptr = [&](u32 k, u32 b) -> const v4u* {
         const bool live = k < nk;
-        const u32 i = b * WB + 4 * lane;
-        const v4u* q = reinterpret_cast<const v4u*>(a.pool + region(k0_ + (live ? k : 0)) * a.region_cap + i);
-        x0 = q[0];                    // unconditional (the pool has AGG_SLACK_UNITS of slack),
-        x1 = q[1];                    // so no branch splits the loads from the waits that let
-        x2 = q[2];                    // the next batch stay in flight
+        const u64 i = (live ? (u64)b * WB : 0) + 4 * lane;
+        return reinterpret_cast<const v4u*>(a.pool + region(k0_ + (live ? k : 0)) * a.region_cap + i);
     };
     auto unit = [](const v4u& x, int h) -> u64 { return h ? ((u64)x.w << 32 | x.z) : ((u64)x.y << 32 | x.x); };
     auto process = [&](u32 k, u32 b, const v4u& x0, const v4u& x1, const v4u& x2) {
@@ -198,10 +220,18 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
         const u32 i0 = b * WB + 4 * lane, len = rlen_s[k];
 #pragma unroll
         for (int j = 0; j < 6; j++) u[j] = i0 + j < len ? u[j] : 0;
+        if (WCG_AGG_ABLATE == 1) { asm volatile("" ::"v"(u[0] ^ u[1] ^ u[2] ^ u[3] ^ u[4] ^ u[5])); return; }
         u64 k0[4], k1[4], c[4];
         bool v[4];
         u32 nu[4];
         agg_decode(u, k0, k1, c, v, nu);
+        if (WCG_AGG_ABLATE == 2) {
+            u32 x = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) x ^= v[j] ? lds_hash(k0[j], k1[j]) + (u32)c[j] : 0u;
+            asm volatile("" ::"v"(x));
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
             typename decltype(tab)::Probe pa, pb;
@@ -211,32 +241,36 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
             if (v[j + 1] && !tab.finish(k0[j + 1], k1[j + 1], pb, c[j + 1])) overflow(k0[j + 1], k1[j + 1], c[j + 1], nu[j + 1]);
         }
     };
-    // NS batches in flight per wave: set s holds the wave's batch P + s; after processing it, it
-    // takes batch P + NS (the set before it, advanced once)
-    constexpr int NS = emit ? 2 : AGG_SETS1;
-    u32 kq[NS], bq[NS];
-    v4u x0[NS], x1[NS], x2[NS];
-    kq[0] = 0; bq[0] = 0;
-    if (per_wave) { kq[0] = wave; bq[0] = (u32)-1; advance(kq[0], bq[0], WSTRIDE); }
-    else advance(kq[0], bq[0], wave);
-#pragma unroll
-    for (int q = 1; q < NS; q++) { kq[q] = kq[q - 1]; bq[q] = bq[q - 1]; advance(kq[q], bq[q], WSTRIDE); }
-#pragma unroll
-    for (int q = 0; q < NS; q++) load(kq[q], bq[q], x0[q], x1[q], x2[q]);
-    bool more = kq[0] < nk;
-    while (more) {
-#pragma unroll
-        for (int q = 0; q < NS; q++) {
-            if (more) {
-                if (kq[q] >= nk) { more = false; continue; }
-                process(kq[q], bq[q], x0[q], x1[q], x2[q]);
-                const int pq = (q + NS - 1) % NS;
-                kq[q] = kq[pq]; bq[q] = bq[pq];
-                advance(kq[q], bq[q], WSTRIDE);
-                load(kq[q], bq[q], x0[q], x1[q], x2[q]);
-            }
-        }
+    // Two batches in flight per wave, in register sets A and B that hold the wave's batches g and
+    // g + 1: the loads are tagged asm and each set's wait counts only the other set's three loads
+    // issued after it (tools/check_inflight.py checks that no copy of an in-flight register sits
+    // between a load and its wait).  The compiler's own wait placement drained both sets at the
+    // top of every batch (s_waitcnt vmcnt(0)), exposing one HBM latency per batch.  Loads are
+    // unconditional (a dead batch reads the first region's first batch), so the count never
+    // depends on which batches are live.  An overflow insert waits for all loads itself (harmless).
+    u32 kA = 0, bA = 0, kB, bB;
+    if (per_wave) { kA = wave; bA = (u32)-1; advance(kA, bA, WSTRIDE); }
+    else advance(kA, bA, wave);
+    kB = kA; bB = bA;
+    advance(kB, bB, WSTRIDE);
+    v4u a0, a1, a2, b0, b1, b2;
+    agg_load_A(batch_ptr(kA, bA), a0, a1, a2);
+    agg_load_B(batch_ptr(kB, bB), b0, b1, b2);
+    while (kA < nk) {
+        agg_wait_A<3>(a0, a1, a2);
+        process(kA, bA, a0, a1, a2);
+        kA = kB; bA = bB;
+        advance(kA, bA, WSTRIDE);
+        agg_load_A(batch_ptr(kA, bA), a0, a1, a2);
+        if (kB >= nk) break;
+        agg_wait_B<3>(b0, b1, b2);
+        process(kB, bB, b0, b1, b2);
+        kB = kA; bB = bA;
+        advance(kB, bB, WSTRIDE);
+        agg_load_B(batch_ptr(kB, bB), b0, b1, b2);
     }
+    agg_wait_A<0>(a0, a1, a2);                        // nothing may land in a dead register
+    agg_wait_B<0>(b0, b1, b2);
     __syncthreads();
     if (!emit) {
         // one-pass mode: the table goes to the global table (one insert per slice and key);
@@ -307,6 +341,7 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     __shared__ u64 wsum[AGG_NT / 64][4];       // per-wave sums (the record log's counts, stats)
     const int tid = threadIdx.x;
     const u32 nb = a.P * a.slices;
+    const u64 t0 = a.clk ? wall_clock64() : 0;
     u64 my_global = 0;
     for (u32 bi = blockIdx.x; bi < nb; bi += gridDim.x)
         my_global += agg_one<MODE>(a, bi, tk0, tk1, tcnt, rlen_s, bstart, spos, wsum);
@@ -324,6 +359,7 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
         u64* dst[4] = {&a.st->tokens, &a.st->lds_hits, &a.st->global_ops, &a.st->long_tokens};
         if (t) atomicAdd(dst[tid], t);
     }
+    if (a.clk && tid == 0) { a.clk[2 * blockIdx.x] = t0; a.clk[2 * blockIdx.x + 1] = wall_clock64(); }
 }
 
 // k_rp (two-pass jobs): workgroup b = (bucket p, slice s) reads the miss-log regions of bucket p

@@ -807,6 +807,34 @@ int reset_tables(wcg_ctx* c) {
     return WCG_OK;
 }
 
+// WCG_AGG_CLOCK diagnostics: k_agg's per-workgroup durations against the miss-log units of
+// its (bucket, slice), printed to stderr
+int agg_clock_report(wcg_ctx* c, const AggArgs& g, u32 nb1, u64 grid) {
+    std::vector<u64> clk(2 * nb1);
+    std::vector<u32> rl(grid * g.P);
+    HIPCHK(c, hipMemcpyAsync(clk.data(), g.clk, clk.size() * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(rl.data(), g.region_len, rl.size() * sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    u64 t0 = ~0ull, t1 = 0;
+    for (u32 b = 0; b < nb1; b++) { t0 = std::min(t0, clk[2 * b]); t1 = std::max(t1, clk[2 * b + 1]); }
+    double sd = 0, su = 0, md = 0, mu = 0;
+    u32 bmax = 0;
+    std::vector<u64> units(nb1, 0);
+    for (u32 bi = 0; bi < nb1; bi++) {
+        const u32 p = bi % g.P, s = bi / g.P;
+        const u32 k0 = (u32)((grid * s) / g.slices), k1 = (u32)((grid * (s + 1)) / g.slices);
+        for (u32 k = k0; k < k1; k++) units[bi] += rl[(u64)k * g.P + p];
+        const double d = (double)(clk[2 * bi + 1] - clk[2 * bi]);
+        sd += d; su += (double)units[bi];
+        if (d > md) { md = d; bmax = bi; }
+        mu = std::max(mu, (double)units[bi]);
+    }
+    fprintf(stderr, "wcg k_agg clock: span %.1f us, wg dur mean %.1f max %.1f us (bi %u: %llu units, start +%.1f us), "
+            "units mean %.0f max %.0f\n", (t1 - t0) / 100.0, sd / nb1 / 100.0, md / 100.0, bmax,
+            (unsigned long long)units[bmax], (clk[2 * bmax] - t0) / 100.0, su / nb1, mu);
+    return WCG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -998,9 +1026,17 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g.spill = nullptr; g.spill_len = nullptr;
     g.emit = c->remit; g.emit_cap = rec_cap_emit;
     g.ovf = nullptr; g.ovf_cap = 0;
+    g.clk = nullptr;
+    static const bool agg_clock = getenv("WCG_AGG_CLOCK") != nullptr;
+    static u64* d_clk = nullptr;
+    if (agg_clock && !two_pass) {          // diagnostics: per-workgroup time against its units
+        if (!d_clk) HIPCHK(c, hipMalloc(&d_clk, 2 * 65536 * sizeof(u64)));
+        g.clk = nb1 <= 65536 ? d_clk : nullptr;
+    }
     if (!two_pass) {
         k_agg<AGG_SPILL><<<nb1, AGG_NT, 0, c->stream>>>(g);
         HIPCHK(c, hipGetLastError());
+        if (g.clk) RC(agg_clock_report(c, g, nb1, grid));
     } else {
     c->two_pass_used = true;
     // k_rp splits each (bucket, slice) of the miss log into AGG_Q sub-buckets; a sub-bucket region

@@ -19,7 +19,10 @@ import sys, os
 sys.path.insert(0, "/root/repo/tools")
 import check_inflight
 name = sys.argv[1]
-e, _, _ = check_inflight.check(open(f"/tmp/var_{name}.s").read(), "_ZN3wcg5k_mapILi0EEEvNS_7MapArgsE")
+text = open(f"/tmp/var_{name}.s").read()
+e = []
+for sym in ("_ZN3wcg5k_mapILi0EEEvNS_7MapArgsE", "_ZN3wcg5k_aggILi0EEEvNS_7AggArgsE", "_ZN3wcg5k_aggILi1EEEvNS_7AggArgsE"):
+    e += check_inflight.check(text, sym)[0]
 if e:
     os.remove(f"/root/repo/build/var/libwcg_{name}.so")
     print(f"variant {name}: REFUSED (in-flight discipline):", *e[:3], sep="\n  ")

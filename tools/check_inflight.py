@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Check the register discipline of k_map's hand-counted asm loads (wcg_common.h).
+"""Check the register discipline of k_map's and k_agg's hand-counted asm loads.
 
 k_map streams its input with inline-asm `buffer_load_dwordx4` and hand-placed `s_waitcnt
 vmcnt(N)`.  The compiler believes an asm output is ready as soon as the asm statement ends, so a
@@ -17,6 +17,9 @@ A value can only move to a different register through a copy, so requiring that 
 tag writes the same registers, and that every wait of a set names exactly those registers
 (A0/A1 for set A, B0/B1 for set B, ...), rules such copies out without any control-flow analysis.
 
+k_agg's batch walk (wcg_agg.h) uses the same tags: sets A and B of three global_load_dwordx4
+each (A0, A1, A2), and waits naming all three registers.
+
 Usage: check_inflight.py FILE.s KERNEL_SYMBOL      (exit status 1 on a violation)
 """
 import re
@@ -26,14 +29,14 @@ import sys
 def kernel_lines(text, sym):
     lines = text.splitlines()
     start = next(i for i, l in enumerate(lines) if l.startswith(sym + ":"))
-    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+    end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
     return lines[start:end + 1]
 
 
 def check(text, sym):
     loads, waits, errors = {}, [], []
     for ln in kernel_lines(text, sym):
-        m = re.search(r"buffer_load_dwordx4\s+(v\[\d+:\d+\]).*wcg-load\s+(\w+)", ln)
+        m = re.search(r"(?:buffer|global)_load_dwordx4\s+(v\[\d+:\d+\]).*wcg-load\s+(\w+)", ln)
         if m:
             loads.setdefault(m.group(2), set()).add(m.group(1))
             continue
