@@ -200,9 +200,10 @@ WCG_API int wcg_merge_runs(wcg_ctx *ctx, const void *dev_text, const uint64_t *r
  * wcg_gather_merge: ms[8] RCCL gather of the runs to root, ms[9] merge of the runs.
  * n = number of doubles the caller provides (<= 10). */
 WCG_API int wcg_timings(wcg_ctx *ctx, double *ms, int n, uint64_t *map_launches);
-/* Enable/disable the event timing above (off by default: it adds event records).  on = 1: the
- * phases of the last job; on = 2: every job from this call on, summed (wcg_reset keeps the events,
- * so a timed loop needs no wcg_timings call, and no host round trip, between its jobs). */
+/* Enable/disable the event timing above (off by default: it adds event records, each a ~5 us
+ * bubble between the kernels it separates).  on = 1: the phases of the last job; on = 2: every job
+ * from this call on, summed (wcg_reset keeps the events, so a timed loop needs no wcg_timings
+ * call, and no host round trip, between its jobs); on = 3: as 2, the map kernel (ms[0]) only. */
 WCG_API int wcg_enable_timing(wcg_ctx *ctx, int on);
 
 /* Diagnostics, stats9 = {tokens, distinct keys, tokens counted in LDS, global-table operations,

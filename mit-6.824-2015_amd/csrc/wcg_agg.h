@@ -36,6 +36,14 @@ constexpr u32 AGG_MAX_SRC = 256;       // source regions per workgroup (+1 KiB L
 constexpr u32 AGG_Q = 128;             // pass-2 sub-buckets per bucket
 constexpr u32 AGG_OVF_CAP = 4096;      // pass 2: overflow records staged per workgroup (128 KiB)
 constexpr int AGG_SPILL = 0, AGG_EMIT = 1;
+#ifndef WCG_AGG_PROBES
+#define WCG_AGG_PROBES 2       // lookups per lane whose LDS reads are in flight together (2; 4 measured no faster: r03_kagg_experiments)
+#endif
+constexpr int AGG_PROBES = WCG_AGG_PROBES;
+#ifndef WCG_AGG_SPEC_K1
+#define WCG_AGG_SPEC_K1 0      // 1: medium keys read their k1 rows with the k0 rows (measured slower on C2 and C4)
+#endif
+constexpr bool AGG_SPEC_K1 = WCG_AGG_SPEC_K1;
 #ifndef WCG_AGG_ABLATE
 #define WCG_AGG_ABLATE 0       // diagnostics: 1 = loads only, 2 = + decode and hash (wrong counts)
 #endif
@@ -232,13 +240,27 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
             asm volatile("" ::"v"(x));
             return;
         }
+        // the AGG_PROBES lookups' row reads issue together (one LDS round trip for them; a
+        // lookup that inserts a key another of the lane's lookups also inserts may leave the key
+        // in two slots: harmless, as between lanes)
+        static_assert(4 % AGG_PROBES == 0, "probe groups split a lane's 4 units");
 #pragma unroll
-        for (int j = 0; j < 4; j += 2) {
-            typename decltype(tab)::Probe pa, pb;
-            if (v[j]) tab.start(emit ? agg_hash(k0[j], k1[j]) : lds_hash(k0[j], k1[j]), pa);
-            if (v[j + 1]) tab.start(emit ? agg_hash(k0[j + 1], k1[j + 1]) : lds_hash(k0[j + 1], k1[j + 1]), pb);
-            if (v[j] && !tab.finish(k0[j], k1[j], pa, c[j])) overflow(k0[j], k1[j], c[j], nu[j]);
-            if (v[j + 1] && !tab.finish(k0[j + 1], k1[j + 1], pb, c[j + 1])) overflow(k0[j + 1], k1[j + 1], c[j + 1], nu[j + 1]);
+        for (int j = 0; j < 4; j += AGG_PROBES) {
+            typename decltype(tab)::Probe pr[AGG_PROBES];
+#pragma unroll
+            for (int q = 0; q < AGG_PROBES; q++) {
+                const u32 h = emit ? agg_hash(k0[j + q], k1[j + q]) : lds_hash(k0[j + q], k1[j + q]);
+                if (!v[j + q]) continue;
+                if (AGG_SPEC_K1) tab.start_k1(h, !key_short(k0[j + q]), pr[q]);
+                else tab.start(h, pr[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < AGG_PROBES; q++) {
+                if (!v[j + q]) continue;
+                const bool ok = AGG_SPEC_K1 ? tab.finish_k1(k0[j + q], k1[j + q], pr[q], c[j + q])
+                                            : tab.finish(k0[j + q], k1[j + q], pr[q], c[j + q]);
+                if (!ok) overflow(k0[j + q], k1[j + q], c[j + q], nu[j + q]);
+            }
         }
     };
     // Two batches in flight per wave, in register sets A and B that hold the wave's batches g and
@@ -342,6 +364,8 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     const int tid = threadIdx.x;
     const u32 nb = a.P * a.slices;
     const u64 t0 = a.clk ? wall_clock64() : 0;
+    // one-pass map calls: compaction's counters start at zero (its memset dispatch cost ~4 us)
+    if (MODE == AGG_SPILL && blockIdx.x == 0 && tid == 0) { a.st->nrec = 0; a.st->nlong = 0; }
     u64 my_global = 0;
     for (u32 bi = blockIdx.x; bi < nb; bi += gridDim.x)
         my_global += agg_one<MODE>(a, bi, tk0, tk1, tcnt, rlen_s, bstart, spos, wsum);
@@ -374,7 +398,10 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
 // together.  The regions belong to this workgroup alone, so their cursors live in LDS too.  A full
 // region falls back to global-table inserts (exact).  Workgroup 0 also adds k_map's per-workgroup
 // stats to DevState (pass 1 does that in one-pass jobs).
-constexpr u32 RP_QB = 96;              // LDS units per sub-bucket buffer (96 KiB in all)
+#ifndef WCG_RP_QB
+#define WCG_RP_QB 96
+#endif
+constexpr u32 RP_QB = WCG_RP_QB;       // LDS units per sub-bucket buffer (96 KiB in all)
 struct RpArgs {
     const u64* pool; const u32* region_len; u64 region_cap;   // the miss log (k_map)
     u32 P, nsrc, slices;                                       // buckets, map workgroups, slices

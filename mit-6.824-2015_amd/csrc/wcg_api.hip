@@ -48,8 +48,8 @@ struct wcg_ctx {
     Rec* crec = nullptr;                      // the compacted records: recA, or the record log
     Rec* sorted = nullptr;                    // recB, or a merge pass's last output
     u64* lens = nullptr; u64 lens_cap = 0;    // per-tile sums of the formatter
-    u64* d_scalar = nullptr;                  // scan totals
-    u64* h_scalar = nullptr;                  // pinned scratch (64 u64)
+    u64* d_scalar = nullptr;                  // scan totals (in st's block, ST_SCALAR_OFF on)
+    u64* h_scalar = nullptr;                  // pinned scratch (64 u64, in h_st's block)
     uint8_t* d_out = nullptr; u64 out_cap = 0; u64 out_len = 0;
     u64 nrec = 0;
     u64 nkeys = 0;                            // distinct keys among the nrec sorted records
@@ -59,6 +59,11 @@ struct wcg_ctx {
     u32* bid = nullptr; u64 bid_cap = 0;
     u64* spx = nullptr; u64 spx_cap = 0;    // sort splitters as arrays (large B)
     bool nkeys_on_device = false;            // the sort's distinct-key count is still in d_scalar[8]
+    // Device-sized reduce (one-pass jobs after the first): compaction, sort and formatting run on
+    // the record count in device memory; c->nrec is the buffers' capacity until wcg_reduce's one
+    // read-back, and the sort is planned for the previous job's count (nrec_hint)
+    bool dev_sized = false;
+    u64 nrec_hint = 0;
     Rec* irec = nullptr; u64 irec_cap = 0;
     LEnt* lent = nullptr; u64 lent_cap = 0;   // long-key partitions: LQ x lpart_cap entries
     u64* spill = nullptr; u64 spill_cap = 0;  // k_agg pass-1 spill regions
@@ -69,6 +74,7 @@ struct wcg_ctx {
     Rec* ovf = nullptr; u64 ovf_cap = 0;      // pass 2's per-workgroup overflow staging
     bool two_pass_used = false;               // a map call since wcg_reset ran the two passes
     bool gtab_zero = false;                   // the global table was cleared by the last wcg_reset
+    u64* glist = nullptr;                     // two-pass contexts: claimed global-table slots
     bool imported = false;                    // wcg_import since wcg_reset
     u32* lpcur = nullptr; u64 lpcur_cap = 0;    // 2n records: by bucket, and the oversized-bucket scratch
     u32* hist = nullptr; u64 hist_cap = 0;    // [B][G] bucket counts / partition counts
@@ -125,6 +131,7 @@ struct wcg_ctx {
     u64 ingest_bytes = 0;                     // bytes mapped by the last wcg_map / wcg_map_file
     // timing
     bool timing = false;
+    bool timing_all = false;                 // every phase (modes 1, 2); mode 3: the map kernel only
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> map_ev, agg_ev;
@@ -243,27 +250,52 @@ int ensure_recs(wcg_ctx* c, u64 n) {
 // record log itself (no copy of the log); otherwise, or when the log's buffer cannot hold them,
 // the log is copied to the front of recA and the tables follow.  The record buffers start at
 // max_keys records and grow (then the compaction runs again) when the tables hold more keys.
-int compact(wcg_ctx* c) {
+int compact(wcg_ctx* c, bool defer = false) {
     if (c->compacted) return WCG_OK;
+    c->dev_sized = false;
+    // wcg_reduce of a one-pass job: no read-back of the count here (a host round trip between
+    // compaction and the sort); the records are bounded by the tables' slots, and the buffers are
+    // sized for that
+    static const bool exact_env = getenv("WCG_EXACT_REDUCE") != nullptr || getenv("WCG_SORT_TARGET") != nullptr;
+    if (defer && !c->two_pass_used && !c->imported && c->nrec_hint >= 2 && !exact_env) {
+        const u64 total = c->gslots + c->lslots;
+        RC(ensure_recs(c, total));
+        // nrec and nlong are zero here: wcg_reset cleared them, and every one-pass map call's
+        // k_agg zeroes them (a tiny memset dispatch costs ~4 us)
+        if (c->timing_all) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
+        k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
+            c->gtab, c->gslots, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st,
+            c->d_scalar + ST_TIE_GROUPS, nullptr);
+        HIPCHK(c, hipGetLastError());
+        if (c->timing_all) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
+        c->nrec = total;                           // a capacity until wcg_reduce reads the count
+        c->crec = c->recA;
+        c->compacted = true;
+        c->dev_sized = true;
+        return WCG_OK;
+    }
     // Two-pass jobs emit their inline keys as records; when nothing else reached the global
     // table (no fallback insert, no import), its slots are all empty and the scan is skipped.
     bool scan_gtab = true;
+    const u64* glist = nullptr;                    // the listed claims instead of the whole table
+    u64 gs = c->gslots;
     if (c->two_pass_used && !c->imported) {
         HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         scan_gtab = c->h_st->global_ops != 0;
+        if (scan_gtab && c->glist && c->h_st->gnew <= GLIST_CAP) { glist = c->glist; gs = c->h_st->gnew; }
     }
-    const u64 gs = scan_gtab ? c->gslots : 0;
+    if (!scan_gtab) gs = 0;
     const u64 total = gs + c->lslots;
     const u64 emit_cap = c->max_keys + 65536;     // the log's length: min(nemit, emit_cap)
     if (c->two_pass_used && c->remit) {
         HIPCHK(c, hipMemsetAsync(&c->st->nlong, 0, sizeof(u64), c->stream));
-        if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
+        if (c->timing_all) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
         k_log_len<<<1, 1, 0, c->stream>>>(emit_cap, c->st);
         k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
-            c->gtab, gs, c->ltab, c->lslots, c->arena, c->remit, c->remit_cap, c->st);
+            c->gtab, gs, c->ltab, c->lslots, c->arena, c->remit, c->remit_cap, c->st, nullptr, glist);
         HIPCHK(c, hipGetLastError());
-        if (c->timing) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
+        if (c->timing_all) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
         RC(check_status(c));
         c->nrec = c->h_st->nrec;
         if (c->nrec <= c->remit_cap) {
@@ -275,15 +307,15 @@ int compact(wcg_ctx* c) {
     }
     for (int pass = 0; pass < 2; pass++) {
         HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));   // nrec, nlong
-        if (c->timing) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
+        if (c->timing_all) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
         if (c->remit && c->two_pass_used)   // the record log of pass 2 first (nrec = nemit; only
                                             // two-pass map calls write it)
             k_copy_emit<<<(unsigned)(c->ncu * 4), 256, 0, c->stream>>>(
                 c->remit, c->recA, std::min<u64>(c->rec_cap, emit_cap), c->st);
         k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
-            c->gtab, gs, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st);
+            c->gtab, gs, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st, nullptr, glist);
         HIPCHK(c, hipGetLastError());
-        if (c->timing) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
+        if (c->timing_all) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
         RC(check_status(c));
         c->nrec = c->h_st->nrec;
         if (c->nrec <= c->rec_cap) break;
@@ -306,7 +338,7 @@ int dbg(wcg_ctx* c, const char* what) {
 // exclusive scan of m u32 in place (multi-block)
 int scan_u32(wcg_ctx* c, u32* v, u64 m) {
     const u64 nb = cdiv(m, SC_SEG);
-    if (nb == 1) {                                 // one segment: one workgroup, one launch
+    if (m <= SC_ONE_MAX) {                         // one workgroup, one launch
         k_scan_apply1<<<1, SC_NT, 0, c->stream>>>(v, m);
         HIPCHK(c, hipGetLastError());
         return WCG_OK;
@@ -349,14 +381,15 @@ int ensure_items(wcg_ctx* c, u64 n2) {
 
 // long keys sharing a 16-byte prefix in r[0:n): ordered by their full bytes (key bytes at
 // `base`); `tmp` is a free record buffer of n records
-int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp) {
+int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64* nd = nullptr) {
     if (n < 2) return WCG_OK;
     RC(ensure(c, &c->groups, &c->groups_cap, n / 2 + 2));
     RC(ensure_items(c, 2 * n));
-    HIPCHK(c, hipMemsetAsync(c->groups, 0, sizeof(u64), c->stream));
-    k_tie_mark<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(r, n, c->groups + 1, c->groups);
+    u64* const ng = c->d_scalar + ST_TIE_GROUPS;   // device-sized jobs: k_compact zeroed it
+    if (!nd) HIPCHK(c, hipMemsetAsync(ng, 0, sizeof(u64), c->stream));
+    k_tie_mark<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(r, n, nd, c->groups, ng);
     TieArgs t;
-    t.r = r; t.n = n; t.base = base; t.groups = c->groups + 1; t.ngroups = c->groups;
+    t.r = r; t.n = n; t.nd = nd; t.base = base; t.groups = c->groups; t.ngroups = ng;
     t.tmp = tmp; t.sc_key = c->ikey; t.sc_pos = c->iidx;
     k_tie_sort<<<(unsigned)c->ncu, TG_NT, 0, c->stream>>>(t);
     HIPCHK(c, hipGetLastError());
@@ -365,11 +398,15 @@ int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp) {
 
 // sample sort of recA[0:nrec) into recB (wcg_sort.h), then the tie groups
 int sort_records(wcg_ctx* c) {
-    const u64 n = c->nrec;
+    // device-sized: n is the capacity (buffers), np the count the launches are planned for
+    const bool dev = c->dev_sized;
+    // (the plan: the previous job's count, but no fewer than 1/16 of the slots, so that a tiny
+    // job followed by a large one does not put the large one into a few oversized buckets)
+    const u64 n = c->nrec, np = dev ? std::min<u64>(std::max<u64>(c->nrec_hint, n / 16), n) : n;
     c->nkeys = n;
     c->sorted = c->recB;
     if (n == 0) return WCG_OK;
-    if (n == 1) {
+    if (n == 1 && !dev) {
         HIPCHK(c, hipMemcpyAsync(c->recB, c->crec, sizeof(Rec), hipMemcpyDeviceToDevice, c->stream));
         return WCG_OK;
     }
@@ -380,23 +417,25 @@ int sort_records(wcg_ctx* c) {
     u64 target = target_env ? target_env : SS_TARGET;
     // small sorts: buckets small enough for two workgroups per CU (C2: 1e5 keys -> 512 buckets
     // of ~200, one-entry networks) rather than fewer buckets than CUs
-    if (!target_env) target = std::min<u64>(target, std::max<u64>(128, cdiv(n, 2ull * c->ncu)));
-    target = std::max<u64>(target, cdiv(n, SS_MAXB));
+    if (!target_env) target = std::min<u64>(target, std::max<u64>(128, cdiv(np, 2ull * c->ncu)));
+    target = std::max<u64>(target, cdiv(np, SS_MAXB));
     SortArgs a;
     a.rec = c->crec; a.n = n; a.out = c->recB;
+    a.nd = dev ? &c->st->nrec : nullptr;
     // the record log: a key may repeat (the global table, other map calls, pass 2's overflow):
-    // the bucket sort merges the copies and counts the distinct keys
-    a.dedupe = c->h_st->nemit != 0;
+    // the bucket sort merges the copies and counts the distinct keys (device-sized jobs are
+    // one-pass: no record log)
+    a.dedupe = !dev && c->h_st->nemit != 0;
     a.nkeys = c->d_scalar + 8;                     // its own slot (the scans use d_scalar[0])
     if (a.dedupe) HIPCHK(c, hipMemsetAsync(a.nkeys, 0, sizeof(u64), c->stream));
-    a.B = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, target), SS_MAXB));
+    a.B = (u32)std::max<u64>(1, std::min<u64>(cdiv(np, target), SS_MAXB));
     // large sorts sample twice as densely: bucket sizes vary as 1/sqrt(samples per bucket), and a
     // bucket past 4 * SB_NT records takes the 8-entry register network (twice the work per record)
     // bucket past 4 * SB_NT records takes the 8-entry register network (twice the work per record);
     // small sorts keep the sample within one workgroup's sort (TS_TILE) when 4+ per bucket allow
     u64 ovs = a.B > SS_LDSB ? 2 * SS_OVS : SS_OVS;
     if (a.B <= SS_LDSB && a.B * ovs > TS_TILE && a.B * 4 <= TS_TILE) ovs = TS_TILE / a.B;
-    a.S = a.B > 1 ? std::min<u64>(n, (u64)a.B * ovs) : 0;
+    a.S = a.B > 1 ? std::min<u64>(np, (u64)a.B * ovs) : 0;
     a.smp = nullptr;
     if (a.B > 1) {
         RC(ensure(c, &c->smp, &c->smp_cap, 2 * a.S));
@@ -414,7 +453,7 @@ int sort_records(wcg_ctx* c) {
     const bool small = a.B <= SS_LDSB;
     // enough workgroups that each thread takes a few records (the bucket search is a chain of
     // dependent reads); the large-B kernels keep one 128 KiB histogram per CU
-    a.G = (u32)std::max<u64>(1, std::min<u64>(cdiv(n, small ? 1024 : 4096), (u64)c->ncu * (small ? 4 : 1)));
+    a.G = (u32)std::max<u64>(1, std::min<u64>(cdiv(np, small ? 1024 : 4096), (u64)c->ncu * (small ? 4 : 1)));
     RC(ensure(c, &c->bid, &c->bid_cap, n));
     RC(ensure(c, &c->hist, &c->hist_cap, (u64)a.B * a.G));
     RC(ensure(c, &c->irec, &c->irec_cap, 2 * n));
@@ -435,7 +474,7 @@ int sort_records(wcg_ctx* c) {
     k_ss_bucket<false><<<a.B, SB_NT, 0, c->stream>>>(a);
     k_ss_bucket<true><<<a.B, SB_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
-    if (c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA));
+    if (dev || c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA, a.nd));
     if (c->crec == c->recA) c->compacted = false;    // recA was scratch for the ties
     if (getenv("WCG_DEBUG"))
         fprintf(stderr, "wcg: nemit %llu global_ops %llu\n", (unsigned long long)c->h_st->nemit,
@@ -450,34 +489,37 @@ int sort_records(wcg_ctx* c) {
 // format records r[0:n) (key bytes of long records at `base`) into *dbuf, `bound` bytes at most;
 // one synchronisation at the end returns the exact size
 int format(wcg_ctx* c, const Rec* r, u64 n, const uint8_t* base, int fmt, u32 nreduce, u32 part, u64 bound,
-           uint8_t** dbuf, u64* cap, u64* nbytes) {
+           uint8_t** dbuf, u64* cap, u64* nbytes, const u64* nd = nullptr) {
     if (n == 0) { *nbytes = 0; return WCG_OK; }
     RC(ensure(c, dbuf, cap, bound + 64));
     const u64 nt = cdiv(n, FM_TILE);
     RC(ensure(c, &c->lens, &c->lens_cap, nt + 1));
     switch (fmt) {
-#define WCG_FMT_SUM(F) case F: k_fmt_sum<F><<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, nreduce, part, base, c->lens); break;
+#define WCG_FMT_SUM(F) case F: k_fmt_sum<F><<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, nd, nreduce, part, base, c->lens); break;
         WCG_FMT_SUM(FMT_MERGED) WCG_FMT_SUM(FMT_JSON) WCG_FMT_SUM(FMT_JSON_ALL) WCG_FMT_SUM(FMT_COPY)
 #undef WCG_FMT_SUM
         default: c->err = "format: unknown format"; return WCG_EINVAL;
     }
     k_scan_u64<<<1, 1024, 0, c->stream>>>(c->lens, nt, c->d_scalar);
     switch (fmt) {
-#define WCG_FMT_WRITE(F) case F: k_fmt_write<F><<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, nreduce, part, base, c->lens, *dbuf); break;
+#define WCG_FMT_WRITE(F) case F: k_fmt_write<F><<<(unsigned)nt, FM_NT, 0, c->stream>>>(r, n, nd, nreduce, part, base, c->lens, *dbuf); break;
         WCG_FMT_WRITE(FMT_MERGED) WCG_FMT_WRITE(FMT_JSON) WCG_FMT_WRITE(FMT_JSON_ALL) WCG_FMT_WRITE(FMT_COPY)
 #undef WCG_FMT_WRITE
     }
     HIPCHK(c, hipGetLastError());
-    // the size, and the sort's distinct-key count (d_scalar[8]) in the same copy
-    HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, 9 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    // the size, and the sort's distinct-key count (d_scalar[8]) in the same copy; device-sized
+    // jobs read the counters (the record count, errors) with them: the job's one round trip
+    if (nd) HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, ST_SCALAR_OFF + 9 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    else HIPCHK(c, hipMemcpyAsync(c->h_scalar, c->d_scalar, 9 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *nbytes = *c->h_scalar;
     return WCG_OK;
 }
 
 u64 merged_bound(wcg_ctx* c, u64 n, bool json) {
-    // inline keys <= 15 bytes; long keys <= 32 bytes in their cell, longer ones on the heap
-    return n * (LONG_CELL + (json ? JSON_FIXED : 3) + 20) + c->h_st->arena_top + 64;
+    // inline keys <= 15 bytes; long keys <= 32 bytes in their cell, longer ones on the heap (its
+    // used part is not known on the host in a device-sized job: the whole heap)
+    return n * (LONG_CELL + (json ? JSON_FIXED : 3) + 20) + (c->dev_sized ? c->arena_cap : c->h_st->arena_top) + 64;
 }
 
 // every -res-<r> for nreduce R, back to back in c->d_part (cached until the next job)
@@ -657,14 +699,28 @@ int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx** 
     HIPCHK(c, hipMalloc(&c->gtab, c->gslots * sizeof(GEntry)));
     HIPCHK(c, hipMalloc(&c->ltab, c->lslots * sizeof(GEntry)));
     HIPCHK(c, hipMalloc(&c->arena, c->lslots * LONG_CELL + c->arena_cap + 64));
-    HIPCHK(c, hipMalloc(&c->st, sizeof(DevState)));
-    HIPCHK(c, hipHostMalloc(&c->h_st, sizeof(DevState), hipHostMallocDefault));
+    // DevState and the scalars (scan totals, the tie-group count) in one block, so that one copy
+    // reads a device-sized job's counters and sizes back
+    static_assert(sizeof(DevState) <= ST_SCALAR_OFF, "DevState fits before the scalars");
+    {
+        uint8_t *d = nullptr, *h = nullptr;
+        HIPCHK(c, hipMalloc(&d, ST_SCALAR_OFF + 64 * sizeof(u64)));
+        HIPCHK(c, hipHostMalloc(&h, ST_SCALAR_OFF + 64 * sizeof(u64), hipHostMallocDefault));
+        c->st = reinterpret_cast<DevState*>(d);
+        c->h_st = reinterpret_cast<DevState*>(h);
+        c->d_scalar = reinterpret_cast<u64*>(d + ST_SCALAR_OFF);
+        c->h_scalar = reinterpret_cast<u64*>(h + ST_SCALAR_OFF);
+        HIPCHK(c, hipMemset(d, 0, ST_SCALAR_OFF + 64 * sizeof(u64)));
+    }
+    // high-cardinality (two-pass) contexts list their few global-table claims (ginsert)
+    if (c->max_keys > (4ull << 20)) {
+        HIPCHK(c, hipMalloc(&c->glist, GLIST_CAP * sizeof(u64)));
+        HIPCHK(c, hipMemcpy(c->d_scalar + ST_GLIST, &c->glist, sizeof(u64*), hipMemcpyHostToDevice));
+    }
     // records: compaction output is bounded by the number of occupied slots
     c->rec_cap = c->max_keys + 65536;
     HIPCHK(c, hipMalloc(&c->recA, c->rec_cap * sizeof(Rec)));
     HIPCHK(c, hipMalloc(&c->recB, c->rec_cap * sizeof(Rec)));
-    HIPCHK(c, hipMalloc(&c->d_scalar, 64 * sizeof(u64)));
-    HIPCHK(c, hipHostMalloc(&c->h_scalar, 64 * sizeof(u64), hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc(&c->h_cur, EX_MAX_RANKS * sizeof(u64), hipHostMallocDefault));
     HIPCHK(c, hipMalloc(&c->d_per_rank, 2 * EX_MAX_RANKS * sizeof(u64)));
     return wcg_reset(c);
@@ -686,16 +742,15 @@ int wcg_close(wcg_ctx* c) {
         if (c->hb[i]) (void)hipHostFree(c->hb[i]);
         if (c->db[i]) (void)hipFree(c->db[i]);
     }
-    void* bufs[] = {c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens, c->d_scalar, c->d_out,
+    void* bufs[] = {c->gtab, c->ltab, c->arena, c->st, c->recA, c->recB, c->lens, c->d_out,
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
                     c->llog, c->llog_len, c->smp, c->bid, c->spx, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->ovf, c->hist, c->spart, c->ikey, c->iidx, c->groups,
                     c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig,
-                    c->d_xcnt, c->xrecv, c->grecv};
+                    c->d_xcnt, c->xrecv, c->grecv, c->glist};
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_xcnt) (void)hipHostFree(c->h_xcnt);
     if (c->h_st) (void)hipHostFree(c->h_st);
-    if (c->h_scalar) (void)hipHostFree(c->h_scalar);
     if (c->h_cur) (void)hipHostFree(c->h_cur);
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -727,8 +782,9 @@ int wcg_set_stream(wcg_ctx* c, void* stream) {
 int wcg_enable_timing(wcg_ctx* c, int on) {
     if (!c) return WCG_EINVAL;
     c->timing = on != 0;
-    c->timing_mode = on == 2 ? 2 : (on ? 1 : 0);
-    if (c->timing_mode == 2) {           // a new accumulation epoch
+    c->timing_all = on == 1 || on == 2;
+    c->timing_mode = on >= 2 && on <= 3 ? on : (on ? 1 : 0);
+    if (c->timing_mode >= 2) {           // a new accumulation epoch
         c->map_ev.clear(); c->agg_ev.clear(); c->phase_jobs.clear(); c->xev.clear();
         c->ev_used = 0; c->map_launches = 0; c->phase_rec = false;
         for (double& v : c->acc) v = 0;
@@ -763,11 +819,11 @@ void sum_events(const wcg_ctx* c, double* acc) {
 }
 
 void record_x(wcg_ctx* c, int phase, hipEvent_t a, hipEvent_t b) {
-    if (c->timing && a && b) c->xev.emplace_back(phase, a, b);
+    if (c->timing_all && a && b) c->xev.emplace_back(phase, a, b);
 }
 
 hipEvent_t mark(wcg_ctx* c) {
-    if (!c->timing) return nullptr;
+    if (!c->timing_all) return nullptr;
     hipEvent_t e = take_event(c);
     return hipEventRecord(e, c->stream) == hipSuccess ? e : nullptr;
 }
@@ -782,19 +838,24 @@ int reset_tables(wcg_ctx* c) {
     // One-pass map calls flush their tables into it, so only after two-pass calls is it worth a
     // host round trip to ask; with no map call since the last clear it is still clear.
     bool clear_g = true;
+    const u64* glist = nullptr;                    // clear only the listed claims
+    u64 g16 = c->gslots * sizeof(GEntry) / 16;
     if (c->gtab_zero && !c->imported) {
         if (c->map_launches_since_reset == 0) clear_g = false;
         else if (c->two_pass_used) {
             HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
             clear_g = c->h_st->global_ops != 0;
+            if (clear_g && c->glist && c->h_st->gnew <= GLIST_CAP) { glist = c->glist; g16 = 2 * c->h_st->gnew; }
         }
     }
     c->map_launches_since_reset = 0;
     // one launch clears the tables and the counters (three memsets were three dispatches)
-    const u64 g16 = clear_g ? c->gslots * sizeof(GEntry) / 16 : 0, l16 = c->lslots * sizeof(GEntry) / 16;
+    if (!clear_g) g16 = 0;
+    const u64 l16 = c->lslots * sizeof(GEntry) / 16;
+    static_assert(sizeof(GEntry) == 32, "k_clear's listed entries are two 16-byte words");
     k_clear<<<grid_for(g16 + l16, 256, c->ncu * 4), 256, 0, c->stream>>>(
-        reinterpret_cast<uint4*>(c->gtab), g16, reinterpret_cast<uint4*>(c->ltab), l16, c->st);
+        reinterpret_cast<uint4*>(c->gtab), g16, reinterpret_cast<uint4*>(c->ltab), l16, c->st, glist);
     HIPCHK(c, hipGetLastError());
     c->gtab_zero = true;
     c->compacted = c->reduced = c->merged = false;
@@ -843,14 +904,14 @@ int wcg_reset(wcg_ctx* c) {
     if (!c) return WCG_EINVAL;
     int rc = set_dev(c);
     if (rc) return rc;
-    if (c->timing_mode == 2 && c->ev_used >= EV_FOLD) {   // recycle the events of earlier jobs
+    if (c->timing_mode >= 2 && c->ev_used >= EV_FOLD) {   // recycle the events of earlier jobs
         HIPCHK(c, hipStreamSynchronize(c->stream));
         sum_events(c, c->acc);
         c->map_ev.clear(); c->agg_ev.clear(); c->phase_jobs.clear(); c->xev.clear();
         c->ev_used = 0;
     }
     RC(reset_tables(c));
-    if (c->timing_mode != 2) {          // mode 2 keeps every job's events until wcg_timings
+    if (c->timing_mode < 2) {           // modes 2, 3 keep every job's events until wcg_timings
         c->map_ev.clear();
         c->agg_ev.clear();
         c->xev.clear();
@@ -1004,8 +1065,10 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         const u64 expect = grid * (u64)a.tiles_per_wg * 16;     // 16 per step: 3x C4's rate
         lp.cap = (u32)std::min<u64>(std::max<u64>(1024, (expect * 5 / 4 + LQ - 1) / LQ), 0x7FFFFFFFull);
         RC(ensure(c, &c->lent, &c->lent_cap, (u64)LQ * lp.cap));
+        u32* const old_cur = c->lpcur;
         RC(ensure(c, &c->lpcur, &c->lpcur_cap, (u64)LQ));
-        HIPCHK(c, hipMemsetAsync(c->lpcur, 0, LQ * sizeof(u32), ls));
+        // k_long_agg leaves every partition cursor at zero for the next map call
+        if (c->lpcur != old_cur) HIPCHK(c, hipMemsetAsync(c->lpcur, 0, LQ * sizeof(u32), ls));
         lp.ent = c->lent; lp.cur = c->lpcur;
         k_long_hash<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, ls>>>(a, lp, (u32)grid);
         k_long_agg<<<LQ, LONG_NT, 0, ls>>>(a, lp);
@@ -1042,19 +1105,23 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // k_rp splits each (bucket, slice) of the miss log into AGG_Q sub-buckets; a sub-bucket region
     // holds 1.5x an even share of what its slice's regions can hold, a full one falls back to
     // exact global inserts
-    const u64 slice_cap = (u64)cdiv(grid, g.slices) * a.region_cap;
+    // k_rp's slices of map workgroups (WCG_RP_SLICES: measurement override)
+    static const char* rps_env = getenv("WCG_RP_SLICES");
+    const u32 sl = rps_env ? std::max<u32>(1, std::min<u32>((u32)grid, (u32)atoi(rps_env))) : g.slices;
+    const u32 nrp = P * sl;
+    const u64 slice_cap = (u64)cdiv(grid, sl) * a.region_cap;
     const u64 cap2 = ((slice_cap * 3 / 2) / AGG_Q + 1024) & ~1ull;
-    RC(ensure(c, &c->pool2, &c->pool2_cap, (u64)nb1 * AGG_Q * cap2 + AGG_SLACK_UNITS));
-    RC(ensure(c, &c->rlen2, &c->rlen2_cap, (u64)nb1 * AGG_Q));
+    RC(ensure(c, &c->pool2, &c->pool2_cap, (u64)nrp * AGG_Q * cap2 + AGG_SLACK_UNITS));
+    RC(ensure(c, &c->rlen2, &c->rlen2_cap, (u64)nrp * AGG_Q));
     RpArgs rp;
     rp.pool = c->pool; rp.region_len = c->region_len; rp.region_cap = a.region_cap;
-    rp.P = P; rp.nsrc = (u32)grid; rp.slices = g.slices; rp.map_stats = c->wg_stats;
+    rp.P = P; rp.nsrc = (u32)grid; rp.slices = sl; rp.map_stats = c->wg_stats;
     rp.pool2 = c->pool2; rp.cap2 = cap2; rp.region_len2 = c->rlen2;
     rp.gtab = c->gtab; rp.gmask = c->gslots - 1; rp.st = c->st;
-    k_rp<<<nb1, AGG_NT, 0, c->stream>>>(rp);
+    k_rp<<<nrp, AGG_NT, 0, c->stream>>>(rp);
     AggArgs g2 = g;
     g2.pool = c->pool2; g2.region_len = c->rlen2; g2.region_cap = cap2;
-    g2.P = P * AGG_Q; g2.nsrc = g.slices; g2.slices = 1;
+    g2.P = P * AGG_Q; g2.nsrc = sl; g2.slices = 1;
     g2.rstride = AGG_Q; g2.rmod = AGG_Q; g2.P1 = P; g2.mode = AGG_EMIT;
     const u32 grid2 = std::min<u32>(P * AGG_Q, (u32)c->ncu * 2);
     g2.ovf_cap = AGG_OVF_CAP;
@@ -1065,10 +1132,12 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     }
     if (fork) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     if (c->timing) {
-        e2 = take_event(c);
-        HIPCHK(c, hipEventRecord(e2, c->stream));
         c->map_ev.push_back({e0, e1});
-        c->agg_ev.push_back({e1, e2});
+        if (c->timing_all) {             // mode 3 times the map kernel only (an event is a ~5 us bubble)
+            e2 = take_event(c);
+            HIPCHK(c, hipEventRecord(e2, c->stream));
+            c->agg_ev.push_back({e1, e2});
+        }
     }
     c->map_launches++;
     c->map_launches_since_reset++;
@@ -1118,14 +1187,23 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
     int rc = set_dev(c);
     if (rc) return rc;
     c->phase_ev[0] = c->phase_ev[1] = nullptr;     // set by compact() only when it runs now
-    RC(compact(c));
+    RC(compact(c, true));
     c->merged = false;
-    if (c->timing) { c->phase_ev[2] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream)); }
+    if (c->timing_all) { c->phase_ev[2] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream)); }
     RC(sort_records(c));
-    if (c->timing) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }
+    if (c->timing_all) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }
     RC(format(c, c->sorted, c->nrec, c->arena, FMT_MERGED, 1, 0, merged_bound(c, c->nrec, false), &c->d_out,
-              &c->out_cap, &c->out_len));
-    if (c->timing) {
+              &c->out_cap, &c->out_len, c->dev_sized ? &c->st->nrec : nullptr));
+    if (c->dev_sized) {                            // the counters came back with the size
+        c->dev_sized = false;
+        c->nrec = c->nkeys = c->h_st->nrec;
+        if (c->h_st->bad_input || c->h_st->overflow || c->h_st->spin_fail) {
+            c->compacted = false;
+            RC(check_status(c));                   // the error message (k_compact wrote nothing)
+        }
+    }
+    c->nrec_hint = c->nrec;
+    if (c->timing_all) {
         c->phase_ev[4] = take_event(c);
         HIPCHK(c, hipEventRecord(c->phase_ev[4], c->stream));
         c->phase_rec = true;
@@ -1592,7 +1670,7 @@ int wcg_timings(wcg_ctx* c, double* ms, int n, uint64_t* map_launches) {
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     double v[10] = {};
-    if (c->timing_mode == 2) {          // summed over every job of the epoch (folded ones too)
+    if (c->timing_mode >= 2) {          // summed over every job of the epoch (folded ones too)
         for (int i = 0; i < 10; i++) v[i] = c->acc[i];
         sum_events(c, v);
     } else {

@@ -71,6 +71,10 @@ __device__ __forceinline__ u64 long_home(u64 s, u64 len, u64 lslots, u64 heap_ca
 }
 
 // ---- device-side counters/status (one per context)
+constexpr u64 ST_SCALAR_OFF = 128;   // the scalars follow DevState in one allocation (wcg_api.hip)
+constexpr u64 ST_TIE_GROUPS = 16;    // scalar slot of the tie-group count (the scans use 0, the sort 8)
+constexpr u64 ST_GLIST = 24;         // scalar slot: two-pass contexts' global-table claim list, or 0
+constexpr u64 GLIST_CAP = 1ull << 20;   // claims listed (more: compaction and reset scan it all)
 struct DevState {
     u64 tokens;          // tokens seen by map kernels
     u64 lds_hits;        // tokens aggregated in LDS
@@ -80,6 +84,7 @@ struct DevState {
     u64 nrec;            // records produced by compaction
     u64 nlong;           // ... of which long keys (> 15 bytes)
     u64 nemit;           // records emitted by k_agg's pass 2 (the record log, across map calls)
+    u64 gnew;            // global-table slots claimed since wcg_reset (two-pass contexts list them)
     u32 overflow;        // table / arena full -> WCG_EFULL
     u32 spin_fail;       // bounded spin gave up -> WCG_EFULL (never expected)
     u32 bad_input;       // malformed record units (wcg_import) or lines (wcg_merge_runs) -> WCG_EINVAL
@@ -342,6 +347,15 @@ __device__ __forceinline__ void ginsert(GEntry* tab, u64 mask, u64 k0, u64 k1, u
             if (cas_agent(&e->k0, &exp, k0)) {
                 if (!shrt) st_agent(&e->k1, k1);
                 add_agent(&e->cnt, cnt);
+                // two-pass contexts keep the global table nearly empty (a few fallback inserts per
+                // GiB) and list its claimed slots, so that compaction and wcg_reset visit those
+                // slots instead of the whole (GB-sized) table
+                u64* const gl = *reinterpret_cast<u64* const*>(reinterpret_cast<const uint8_t*>(st) + ST_SCALAR_OFF +
+                                                               ST_GLIST * sizeof(u64));
+                if (gl) {
+                    const u64 i = atomicAdd((unsigned long long*)&st->gnew, 1ull);
+                    if (i < GLIST_CAP) gl[i] = s;
+                }
                 return;
             }
             c0 = exp;

@@ -31,6 +31,7 @@ struct LdsTable {
     struct Probe {
         u32 b1, b2;
         u64 v[W], w[W];
+        u64 v1[W], w1[W];     // start_k1: the k1 rows too (medium keys)
     };
 
     __device__ __forceinline__ void init(int tid, int nt) {
@@ -67,7 +68,45 @@ struct LdsTable {
         readrow(p.b2, p.w);
     }
 
+    // the same, with both buckets' k1 rows read in the same round trip when the key has 8+ bytes
+    // (finish_k1 then confirms a k0 match without a dependent read)
+    __device__ __forceinline__ void start_k1(u32 h, bool med, Probe& p) const {
+        buckets(h, p.b1, p.b2);
+        readrow(p.b1, p.v);
+        readrow(p.b2, p.w);
+        if (med) {
+            const uint4* q1 = reinterpret_cast<const uint4*>(&k1[p.b1][0]);
+            const uint4* q2 = reinterpret_cast<const uint4*>(&k1[p.b2][0]);
+#pragma unroll
+            for (int q = 0; q < W / 2; q++) {
+                const uint4 x = q1[q], y = q2[q];
+                p.v1[2 * q] = (u64)x.y << 32 | x.x; p.v1[2 * q + 1] = (u64)x.w << 32 | x.z;
+                p.w1[2 * q] = (u64)y.y << 32 | y.x; p.w1[2 * q + 1] = (u64)y.w << 32 | y.z;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < W; j++) { p.v1[j] = 0; p.w1[j] = 0; }
+        }
+    }
+
     __device__ __forceinline__ void add_cnt(u32 b, int j, CNT c) { atomicAdd(&cnt[b][j], c); }
+
+    // finish() after start_k1: a match is decided from the rows already read (short keys have
+    // k1 == 0 and compare with the zeros start_k1 put there); the insert path is finish()'s
+    __device__ __forceinline__ bool finish_k1(u64 a0, u64 a1, const Probe& p, CNT c) {
+        u32 m = 0;
+#pragma unroll
+        for (int j = 0; j < W; j++) {
+            m |= (u32)(p.v[j] == a0 && p.v1[j] == a1) << j;
+            m |= (u32)(p.w[j] == a0 && p.w1[j] == a1) << (W + j);
+        }
+        if (m) {
+            const int s = __ffs(m) - 1;
+            add_cnt(s < W ? p.b1 : p.b2, s % W, c);
+            return true;
+        }
+        return finish(a0, a1, p, c);
+    }
 
     // match (slot s: bucket b1 for s < W, else b2; way s % W) or insert; false when both
     // buckets are full of other keys.  Straight-line common path: bit masks and one atomic at a

@@ -490,6 +490,7 @@ __global__ __launch_bounds__(LONG_NT) void k_long_agg(MapArgs a, LongPart lp) {
         const u64 rr = srec[s], len = rr >> 40, p = rr & LLOG_OFF_MASK;
         ltab_add(a, len, long_tag(sh[s], len), [&](u64 j) -> u32 { return input_word(a, p, (u32)len, j); }, c, false);
     }
+    if (threadIdx.x == 0) lp.cur[q] = 0;      // for the next map call (every thread read it long ago)
 }
 
 // wave-local ordering of LDS accesses between lanes (the LDS executes one wave's
@@ -506,10 +507,21 @@ __device__ __forceinline__ void wave_lds_sync() {
 // s_waitcnt): one asm keeps the set's registers in place (a chain of C++ branches, each with
 // its own asm, makes the compiler merge their outputs through register copies)
 #define WCG_W1(N, L) "s_cmp_ge_u32 %1, " #N "\n\ts_cbranch_scc0 " #L "f\n\ts_waitcnt vmcnt(" #N ")\n\ts_branch 99f\n" #L ":\n\t"
+#ifndef WCG_WAIT_FIRST
+#define WCG_WAIT_FIRST 1                     // try vmcnt(14) first (steady state: one compare); 0: the full chain
+#endif
+#if WCG_WAIT_FIRST
+// steady state: n >= 14 (3 loads + >= 2 stores per step), so the first compare decides; vmcnt(14)
+// leaves the last two steps' windows in flight (2 vs 4 sets in flight measured equal in r02)
+#define WCG_WAIT_CHAIN(TAG)                                                                     \
+    WCG_W1(14, 86) WCG_W1(12, 87) WCG_W1(10, 88) WCG_W1(8, 89) WCG_W1(6, 90) WCG_W1(4, 91)      \
+    WCG_W1(2, 92) "s_waitcnt vmcnt(0)\n99: ; " TAG
+#else
 #define WCG_WAIT_CHAIN(TAG)                                                                     \
     WCG_W1(48, 81) WCG_W1(36, 82) WCG_W1(28, 83) WCG_W1(22, 84) WCG_W1(18, 85) WCG_W1(14, 86)   \
     WCG_W1(12, 87) WCG_W1(10, 88) WCG_W1(8, 89) WCG_W1(6, 90) WCG_W1(4, 91) WCG_W1(2, 92)        \
     "s_waitcnt vmcnt(0)\n99: ; " TAG
+#endif
 #define WCG_SET_OPS(S)                                                                          \
     __device__ __forceinline__ void set_load_##S(v4i rsrc, u32 om, v4u& m) {                    \
         /* s_nop 4: the descriptor SGPRs may have just been written by a VALU readfirstlane */    \

@@ -22,10 +22,17 @@ constexpr int CP_NT = 256, CP_IPT = 8;          // 2048 table slots per block, o
 
 // Each thread takes CP_IPT slots: every slot entry is loaded first, unconditionally (a load in a
 // per-slot branch made a serial chain of memory latencies), then long keys' 16-byte prefixes.
+// glist (two-pass jobs): the gtab part is the gslots listed slots gtab[glist[i]], not gtab[0, gslots)
 __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
-                                                  const uint8_t* arena, Rec* out, u64 cap, DevState* st) {
+                                                  const uint8_t* arena, Rec* out, u64 cap, DevState* st, u64* zero,
+                                                  const u64* glist) {
+    if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;   // a later kernel's counter
     __shared__ u32 wsum[CP_NT / 64], wlong[CP_NT / 64];
     __shared__ u64 base_s;
+    // a failed job (full table or arena, malformed import) compacts nothing: its slots may hold
+    // half-published long keys (no arena offset), and the reduce's sort and formatting may run
+    // before the host reads the error (device-sized jobs)
+    if (st->overflow | st->spin_fail | st->bad_input) return;
     const u64 total = gslots + lslots;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u64 b0 = (u64)blockIdx.x * CP_NT * CP_IPT;
@@ -33,7 +40,7 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
 #pragma unroll
     for (int j = 0; j < CP_IPT; j++) {
         const u64 i = b0 + (u64)j * CP_NT + tid;
-        const GEntry* src = i < gslots ? gtab + i : ltab + (i < total ? i - gslots : lslots - 1);
+        const GEntry* src = i < gslots ? gtab + (glist ? glist[i] : i) : ltab + (i < total ? i - gslots : lslots - 1);
         e[j] = *src;
         if (i >= total) e[j].k0 = 0;
     }
@@ -87,12 +94,13 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
         if (have & (1u << j)) { if (pos < cap) out[pos] = r[j]; pos++; }   // more: host grows, reruns
 }
 
-// wcg_reset: zero n1 + n2 16-byte words of two tables and the DevState counters, one dispatch
-__global__ void k_clear(uint4* t1, u64 n1, uint4* t2, u64 n2, DevState* st) {
+// wcg_reset: zero n1 + n2 16-byte words of two tables and the DevState counters, one dispatch;
+// with list1 the first table's part is the n1 / 2 listed 32-byte entries t1[2 list1[i] + {0, 1}]
+__global__ void k_clear(uint4* t1, u64 n1, uint4* t2, u64 n2, DevState* st, const u64* list1) {
     const uint4 z = make_uint4(0, 0, 0, 0);
     const u64 stride = (u64)gridDim.x * blockDim.x;
     for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n1 + n2; i += stride) {
-        if (i < n1) t1[i] = z; else t2[i - n1] = z;
+        if (i < n1) t1[list1 ? 2 * list1[i >> 1] + (i & 1) : i] = z; else t2[i - n1] = z;
     }
     if (blockIdx.x == 0) {
         u32* w = reinterpret_cast<u32*>(st);
@@ -186,16 +194,19 @@ __device__ __forceinline__ u64 block_excl_scan(u64 s, u64* ws, u64& all) {
 }
 
 // a thread's FM_IPT records, loaded unconditionally (a load inside a per-record branch was a
-// serial chain of memory latencies); records past n are returned with count 0 and are not used
+// serial chain of memory latencies); records past n are not used
 __device__ __forceinline__ void fmt_load(const Rec* r, u64 n, u64 i0, Rec* x) {
 #pragma unroll
-    for (int k = 0; k < FM_IPT; k++) x[k] = r[i0 + k < n ? i0 + k : n - 1];
+    for (int k = 0; k < FM_IPT; k++) x[k] = r[i0 + k < n ? i0 + k : (n ? n - 1 : 0)];
 }
+// device-sized formatting: n is the capacity the tiles were launched for, *nd the records
+__device__ __forceinline__ u64 fmt_count(u64 n, const u64* nd) { return nd && *nd < n ? *nd : n; }
 
 template <int FMT>
-__global__ __launch_bounds__(FM_NT) void k_fmt_sum(const Rec* r, u64 n, u32 nreduce, u32 part, const uint8_t* arena,
-                                                  u64* tsum) {
+__global__ __launch_bounds__(FM_NT) void k_fmt_sum(const Rec* r, u64 n, const u64* nd, u32 nreduce, u32 part,
+                                                  const uint8_t* arena, u64* tsum) {
     __shared__ u64 ws[FM_NT / 64];
+    n = fmt_count(n, nd);
     const u64 i0 = (u64)blockIdx.x * FM_TILE + (u64)threadIdx.x * FM_IPT;
     Rec x[FM_IPT];
     fmt_load(r, n, i0, x);
@@ -250,10 +261,11 @@ __device__ __forceinline__ void fmt_lines(const Rec* x, const u64* L, const uint
 // (dst & 15).  A tile larger than the stage (long keys) writes its bytes directly.
 constexpr u32 FM_STAGE = 32768;
 template <int FMT>
-__global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, u32 nreduce, u32 part, const uint8_t* arena,
-                                                    const u64* toff, uint8_t* out) {
+__global__ __launch_bounds__(FM_NT) void k_fmt_write(const Rec* r, u64 n, const u64* nd, u32 nreduce, u32 part,
+                                                    const uint8_t* arena, const u64* toff, uint8_t* out) {
     __shared__ u64 ws[FM_NT / 64];
     __shared__ __align__(16) uint8_t sb[FM_STAGE];
+    n = fmt_count(n, nd);
     const u64 i0 = (u64)blockIdx.x * FM_TILE + (u64)threadIdx.x * FM_IPT;
     Rec x[FM_IPT];
     fmt_load(r, n, i0, x);

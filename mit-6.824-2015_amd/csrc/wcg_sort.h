@@ -342,26 +342,34 @@ __global__ __launch_bounds__(SC_NT) void k_scan_apply(u32* v, u64 n, const u64* 
     }
 }
 
-// a single segment (m <= SC_SEG): exclusive scan from 0
+// one segment (m <= SC_ONE_MAX): one workgroup (walking several segments in order with a running
+// carry took 49 us on C2's 50K-entry histogram, against 18 us for the three-kernel scan: each
+// segment waits for its loads in turn)
+constexpr u64 SC_ONE_MAX = SC_SEG;
 __global__ __launch_bounds__(SC_NT) void k_scan_apply1(u32* v, u64 m) {
     __shared__ u64 ws[SC_NT / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const u64 base = (u64)tid * SC_IPT;
-    u32 x[SC_IPT];
-    u64 s = 0;
+    u64 carry = 0;
+    for (u64 seg = 0; seg < m; seg += SC_SEG) {
+        const u64 base = seg + (u64)tid * SC_IPT;
+        u32 x[SC_IPT];
+        u64 s = 0;
 #pragma unroll
-    for (int k = 0; k < SC_IPT; k++) { x[k] = base + k < m ? v[base + k] : 0u; s += x[k]; }
-    u64 incl = s;
-    for (int d = 1; d < 64; d <<= 1) { const u64 y = __shfl_up(incl, d, 64); if (lane >= d) incl += y; }
-    if (lane == 63) ws[w] = incl;
-    __syncthreads();
-    u64 pre = 0;
-    for (int k = 0; k < w; k++) pre += ws[k];
-    u64 run = pre + incl - s;
+        for (int k = 0; k < SC_IPT; k++) { x[k] = base + k < m ? v[base + k] : 0u; s += x[k]; }
+        u64 incl = s;
+        for (int d = 1; d < 64; d <<= 1) { const u64 y = __shfl_up(incl, d, 64); if (lane >= d) incl += y; }
+        if (lane == 63) ws[w] = incl;
+        __syncthreads();
+        u64 pre = 0, all = 0;
+        for (int k = 0; k < SC_NT / 64; k++) { if (k < w) pre += ws[k]; all += ws[k]; }
+        u64 run = carry + pre + incl - s;
 #pragma unroll
-    for (int k = 0; k < SC_IPT; k++) {
-        if (base + k < m) v[base + k] = (u32)run;
-        run += x[k];
+        for (int k = 0; k < SC_IPT; k++) {
+            if (base + k < m) v[base + k] = (u32)run;
+            run += x[k];
+        }
+        carry += all;
+        __syncthreads();                  // ws is rewritten by the next segment
     }
 }
 
@@ -388,7 +396,9 @@ constexpr int SS_U = WCG_SS_U;         // records per thread in flight (hist / s
 
 struct SortArgs {
     const Rec* rec;          // compacted records (index = position)
-    u64 n;
+    u64 n;                   // records, or (nd set) the buffers' capacity
+    const u64* nd;           // device-sized sorts: the record count in device memory (<= n), so
+                             // that the host plans the launches without reading it back
     const Rec* smp;          // sorted sample: hi, lo, cnt = record index
     u64 S;                   // samples
     u32 B;                   // buckets
@@ -404,12 +414,16 @@ struct SortArgs {
                                     // searches' global reads stay within 20 B per splitter (L2)
 };
 
+// the records to sort: a.n, or the count the device holds (a plan made for another count only
+// changes the buckets' sizes: samples repeat when S > n, and buckets may be empty or oversized)
+__device__ __forceinline__ u64 ss_count(const SortArgs& a) { return a.nd ? (*a.nd < a.n ? *a.nd : a.n) : a.n; }
+
 // sample j = record floor(j * n / S): stored in index order, so a stable sort gives the
 // (hi, lo, index) order
 __global__ void k_ss_sample(SortArgs a, Rec* smp) {
     const u64 j = blockIdx.x * (u64)blockDim.x + threadIdx.x;
     if (j >= a.S) return;
-    const u64 i = j * a.n / a.S;
+    const u64 i = j * ss_count(a) / a.S;
     const Rec r = a.rec[i];
     Rec s;
     s.hi = r.hi; s.lo = r.lo; s.cnt = i; s.ref = 0;
@@ -430,8 +444,9 @@ __global__ void k_ss_split(SortArgs a) {
 }
 
 __device__ __forceinline__ void ss_range(const SortArgs& a, u64& i0, u64& i1) {
-    i0 = a.n * blockIdx.x / a.G;
-    i1 = a.n * (blockIdx.x + 1) / a.G;
+    const u64 n = ss_count(a);
+    i0 = n * blockIdx.x / a.G;
+    i1 = n * (blockIdx.x + 1) / a.G;
 }
 
 // Up to SS_LDSB buckets every splitter is staged in LDS (a binary search of LDS reads), and the
@@ -568,8 +583,9 @@ constexpr int RK_NT = 256, RK_SPB = RK_NT / 64;   // samples per block: one per 
 __global__ __launch_bounds__(RK_NT) void k_ss_rank_sort(SortArgs a, Rec* smp) {
     __shared__ u64 sh[TS_TILE], sl[TS_TILE];
     const u32 S = (u32)a.S;
+    const u64 n = ss_count(a);
     for (u32 j = threadIdx.x; j < S; j += RK_NT) {
-        const Rec& r = a.rec[j * a.n / S];
+        const Rec& r = a.rec[j * n / S];
         sh[j] = r.hi; sl[j] = r.lo;
     }
     __syncthreads();
@@ -582,7 +598,7 @@ __global__ __launch_bounds__(RK_NT) void k_ss_rank_sort(SortArgs a, Rec* smp) {
     for (int d = 32; d >= 1; d >>= 1) rank += __shfl_xor((int)rank, d, 64);
     if (lane != 0) return;
     Rec o;
-    o.hi = h; o.lo = l; o.cnt = (u64)j * a.n / S; o.ref = 0;
+    o.hi = h; o.lo = l; o.cnt = (u64)j * n / S; o.ref = 0;
     smp[rank] = o;
 }
 
@@ -734,7 +750,7 @@ __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
     __shared__ uint16_t kp[CAP];
     const u32 b = blockIdx.x;
     const u64 s = a.hist[(u64)b * a.G];
-    const u64 e = b + 1 < a.B ? a.hist[(u64)(b + 1) * a.G] : a.n;
+    const u64 e = b + 1 < a.B ? a.hist[(u64)(b + 1) * a.G] : ss_count(a);
     const u64 m = e - s;
     if (m == 0 || (m > 4 * SB_NT) != BIG) return;
     if (m > SB_CAP) { ss_global_sort(a, s, m, kh, kl, kp); return; }
@@ -793,7 +809,8 @@ __device__ __forceinline__ bool same_prefix(const Rec& x, const Rec& y) { return
 
 // group starts: long keys whose successor shares their 16-byte prefix and whose predecessor
 // does not
-__global__ void k_tie_mark(const Rec* r, u64 n, u64* groups, u64* ngroups) {
+__global__ void k_tie_mark(const Rec* r, u64 n, const u64* nd, u64* groups, u64* ngroups) {
+    if (nd && *nd < n) n = *nd;                  // device-sized: the sorted records only
     for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i + 1 < n; i += (u64)gridDim.x * blockDim.x) {
         const Rec x = r[i], y = r[i + 1];
         if (!rec_long(x) || !rec_long(y) || !same_prefix(x, y)) continue;
@@ -814,7 +831,8 @@ constexpr u32 TG_CAP = 2048;
 
 struct TieArgs {
     Rec* r;                // sorted records
-    u64 n;
+    u64 n;                 // records, or (nd set) the capacity
+    const u64* nd;         // device-sized: the record count in device memory
     const uint8_t* base;   // key bytes of long records
     const u64* groups;
     const u64* ngroups;
@@ -837,6 +855,7 @@ __global__ __launch_bounds__(TG_NT) void k_tie_sort(TieArgs a) {
     __shared__ u64 end_s;
     const int tid = threadIdx.x;
     const u64 ng = *a.ngroups;
+    if (a.nd && *a.nd < a.n) a.n = *a.nd;
     for (u64 g = blockIdx.x; g < ng; g += gridDim.x) {
         const u64 s = a.groups[g];
         const Rec x0 = a.r[s];

@@ -169,8 +169,9 @@ class Engine:
 
     def enable_timing(self, on=True) -> None:
         """on = True/1: phase times of the last job; 2: summed over every job from now on (no
-        timings() call, hence no host round trip, needed between jobs); False/0: off."""
-        mode = 2 if on == 2 and on is not True else (1 if on else 0)
+        timings() call, hence no host round trip, needed between jobs); 3: as 2, the map kernel
+        only (each event is a ~5 us bubble between kernels); False/0: off."""
+        mode = on if on in (2, 3) and on is not True else (1 if on else 0)
         self._chk(self._lib.wcg_enable_timing(self._ctx, mode))
 
     # -- phases
