@@ -45,7 +45,7 @@ constexpr int AGG_PROBES = WCG_AGG_PROBES;
 #endif
 constexpr bool AGG_SPEC_K1 = WCG_AGG_SPEC_K1;
 #ifndef WCG_AGG_ABLATE
-#define WCG_AGG_ABLATE 0       // diagnostics: 1 = loads only, 2 = + decode and hash (wrong counts)
+#define WCG_AGG_ABLATE 0       // diagnostics: 1 = loads only, 2 = + decode and hash, 3 = no flush (wrong counts)
 #endif
 
 struct AggArgs {
@@ -300,7 +300,7 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
         // pass-2 sub-bucket and is emitted once per map call (no duplicate with the global table)
         for (int i = tid; i < AGG_NB * AGG_W; i += AGG_NT) {
             const u64 c = (&tcnt[0][0])[i];
-            if (!c) continue;
+            if (!c || WCG_AGG_ABLATE == 3) continue;     // 3: no flush (diagnostics: wrong counts)
             const u64 k0 = (&tk0[0][0])[i], k1 = (&tk1[0][0])[i];
             if (a.spill_cap) { overflow(k0, k1, c, (u32)entry_units(k0, (u32)(c > 1 ? 2 : 1))); continue; }
             my_global++;
@@ -399,9 +399,10 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
 // region falls back to global-table inserts (exact).  Workgroup 0 also adds k_map's per-workgroup
 // stats to DevState (pass 1 does that in one-pass jobs).
 #ifndef WCG_RP_QB
-#define WCG_RP_QB 96
+#define WCG_RP_QB 48
 #endif
-constexpr u32 RP_QB = WCG_RP_QB;       // LDS units per sub-bucket buffer (96 KiB in all)
+constexpr u32 RP_QB = WCG_RP_QB;       // LDS units per sub-bucket buffer (48 KiB in all: two k_rp
+                                       // workgroups per CU; 96 measured 6% slower on C4)
 struct RpArgs {
     const u64* pool; const u32* region_len; u64 region_cap;   // the miss log (k_map)
     u32 P, nsrc, slices;                                       // buckets, map workgroups, slices

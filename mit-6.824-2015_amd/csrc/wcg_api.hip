@@ -4,6 +4,7 @@
 // (tables, records) or on first need (sort items, staging), sized for 288 GB HBM parts: the
 // aggregation tables, the record buffers for the sort and the formatted output all stay
 // resident, so a job is a fixed sequence of launches on one stream.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -1016,18 +1017,24 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     HIPCHK(c, hipMemsetAsync(d_stamps, 0, MAP_NSTAMP * sizeof(u64), c->stream));
     a.stamps = d_stamps;
 #endif
+    // timing: the kernel's own start / end timestamps through hipExtLaunchKernel (events recorded
+    // as separate stream markers cost a ~5 us bubble each between the kernels around them)
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-    if (c->timing) { e0 = take_event(c); HIPCHK(c, hipEventRecord(e0, c->stream)); }
+    if (c->timing) { e0 = take_event(c); e1 = take_event(c); }
     static const int ablate = getenv("WCG_MAP_ABLATE") ? atoi(getenv("WCG_MAP_ABLATE")) : 0;
+    auto launch = [&](auto kern) {
+        if (e0) hipExtLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(MAP_NT), 0, c->stream, e0, e1, 0u, a);
+        else kern<<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a);
+    };
     switch (ablate) {
-        case 1: k_map<1><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
-        case 2: k_map<2><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
-        case 3: k_map<3><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
-        case 4: k_map<4><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
-        case 5: k_map<5><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
-        case 6: k_map<6><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
-        case 7: k_map<7><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
-        default: k_map<0><<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a); break;
+        case 1: launch(k_map<1>); break;
+        case 2: launch(k_map<2>); break;
+        case 3: launch(k_map<3>); break;
+        case 4: launch(k_map<4>); break;
+        case 5: launch(k_map<5>); break;
+        case 6: launch(k_map<6>); break;
+        case 7: launch(k_map<7>); break;
+        default: launch(k_map<0>); break;
     }
     HIPCHK(c, hipGetLastError());
 #if WCG_STAMPS
@@ -1041,7 +1048,6 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
                 h[3] / ns, h[4] / ns, h[5] / ns);
     }
 #endif
-    if (c->timing) { e1 = take_event(c); HIPCHK(c, hipEventRecord(e1, c->stream)); }
     // the logged long tokens: hashed into LQ partitions (LONG_PARTS workgroups per map
     // workgroup's region), then one workgroup per partition.  Partition capacity: the log's
     // capacity spread evenly, with slack (the LDS cache folds hot keys before they are emitted;
@@ -1105,9 +1111,11 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // k_rp splits each (bucket, slice) of the miss log into AGG_Q sub-buckets; a sub-bucket region
     // holds 1.5x an even share of what its slice's regions can hold, a full one falls back to
     // exact global inserts
-    // k_rp's slices of map workgroups (WCG_RP_SLICES: measurement override)
+    // k_rp's slices of map workgroups: twice pass 1's, so that k_rp's 52 KiB workgroups run two
+    // per CU (C4 1 GiB: aggregation 3.71 -> 3.49 ms against one 100 KiB workgroup per CU,
+    // profiles/r03_kagg_experiments/rp_slices.txt; WCG_RP_SLICES: measurement override)
     static const char* rps_env = getenv("WCG_RP_SLICES");
-    const u32 sl = rps_env ? std::max<u32>(1, std::min<u32>((u32)grid, (u32)atoi(rps_env))) : g.slices;
+    const u32 sl = std::max<u32>(1, std::min<u32>((u32)grid, rps_env ? (u32)atoi(rps_env) : 2 * g.slices));
     const u32 nrp = P * sl;
     const u64 slice_cap = (u64)cdiv(grid, sl) * a.region_cap;
     const u64 cap2 = ((slice_cap * 3 / 2) / AGG_Q + 1024) & ~1ull;
