@@ -33,8 +33,11 @@ HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    # k_map's launch time falls over its first ~10 launches on a fresh process (978 -> 890 us in
+    # profiles/r03_kernel_trace_v8: clocks and page tables warming up), so the default warm-up
+    # covers that; a step is ~1.3 ms, the whole default run is dominated by corpus generation
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=15)
     ap.add_argument("--workload", default=None,
                     help="default: c2_ascii_zipf_1gib at N = 1 (BASELINE config 2, the metric's config); "
                          "c3_ascii_zipf_16gib at N > 1 (BASELINE config 3: 16 GiB strong-scaled over N, nReduce 64)")
