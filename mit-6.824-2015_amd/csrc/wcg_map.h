@@ -57,6 +57,9 @@ constexpr int MAP_SST = 512;                 // max token starts per step (992 /
 #ifndef WCG_DIRECT
 #define WCG_DIRECT 0                         // 1: no start list (measured slower: r03_kmap_experiments)
 #endif
+#ifndef WCG_KEYREAD4
+#define WCG_KEYREAD4 1                       // key bytes by dword reads from rp & ~3 (0: b64 pairs)
+#endif
 #ifndef WCG_ADMIT2
 #define WCG_ADMIT2 1                         // k_map LDS tables admit keys on their second miss
 #endif
@@ -639,21 +642,36 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
     // ---- token decoding.  An entry of the start list -> the key's 16 bytes from three aligned
     //      8-byte LDS reads (unaligned 8-byte LDS reads cost ~20x the LDS cycles), then the key
     //      identity of fact F4 with byte masks, and its LDS hash
-    struct KeyWords { uint2 q0, q1, q2; };
     struct Tok { u32 e, k0l, k0h, k1l, k1h, h; bool shrt, lng, valid; };
+#if WCG_KEYREAD4
+    // r03: the key's dwords from rp & ~3 (dword reads: ds_read2_b32 pairs), so the word at rp is
+    // one alignbyte away; 8-byte-aligned pairs needed a select of every dword by rp & 4
+    struct KeyWords { u32 d0, d1, d2, d3, d4; };
+    auto keyread = [&](u32 e) -> KeyWords {
+        const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1);
+        const u32* q = reinterpret_cast<const u32*>(bytes + (rp & ~3u));
+        return KeyWords{q[0], q[1], q[2], q[3], q[4]};
+    };
+#else
+    struct KeyWords { uint2 q0, q1, q2; };
     auto keyread = [&](u32 e) -> KeyWords {
         const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1);
         const uint2* q = reinterpret_cast<const uint2*>(bytes + (rp & ~7u));
         return KeyWords{q[0], q[1], q[2]};
     };
+#endif
     auto decode_tok = [&](u32 e, bool act, const KeyWords& kw) -> Tok {
         Tok t;
         t.e = e;
         const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1), len = e >> SST_LEN_SHIFT;
         const u32 bsh = rp & 3u;
+#if WCG_KEYREAD4
+        const u32 e0 = kw.d0, e1 = kw.d1, e2 = kw.d2, e3 = kw.d3, e4 = kw.d4;
+#else
         const bool hi4 = (rp & 4u) != 0;
         const u32 e0 = hi4 ? kw.q0.y : kw.q0.x, e1 = hi4 ? kw.q1.x : kw.q0.y, e2 = hi4 ? kw.q1.y : kw.q1.x;
         const u32 e3 = hi4 ? kw.q2.x : kw.q1.y, e4 = hi4 ? kw.q2.y : kw.q2.x;
+#endif
         const u32 w0 = __builtin_amdgcn_alignbyte(e1, e0, bsh), w1 = __builtin_amdgcn_alignbyte(e2, e1, bsh);
         const u32 w2 = __builtin_amdgcn_alignbyte(e3, e2, bsh), w3 = __builtin_amdgcn_alignbyte(e4, e3, bsh);
         // keep the key's bytes: nb = bytes in the last (partial) word pair, 0..7
@@ -772,16 +790,25 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
             // short key (<= 7 bytes): its bytes lie in [rp & ~7, +16): two aligned 8-byte reads
             auto keyread_s = [&](u32 e) -> uint4 {
                 const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1);
+#if WCG_KEYREAD4
+                const u32* q = reinterpret_cast<const u32*>(bytes + (rp & ~3u));
+                return make_uint4(q[0], q[1], q[2], 0u);
+#else
                 const uint2* q = reinterpret_cast<const uint2*>(bytes + (rp & ~7u));
                 const uint2 x = q[0], y = q[1];
                 return make_uint4(x.x, x.y, y.x, y.y);
+#endif
             };
             struct TokS { u64 k; u32 h; };
             auto decode_s = [&](u32 e, const uint4& kw) -> TokS {
                 const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1), len = e >> SST_LEN_SHIFT;
                 const u32 bsh = rp & 3u;
+#if WCG_KEYREAD4
+                const u32 e0 = kw.x, e1 = kw.y, e2 = kw.z;
+#else
                 const bool hi4 = (rp & 4u) != 0;
                 const u32 e0 = hi4 ? kw.y : kw.x, e1 = hi4 ? kw.z : kw.y, e2 = hi4 ? kw.w : kw.z;
+#endif
                 const u64 w = (u64)__builtin_amdgcn_alignbyte(e2, e1, bsh) << 32 | __builtin_amdgcn_alignbyte(e1, e0, bsh);
                 TokS t;
                 t.k = (w & ((1ull << (8 * len)) - 1)) | (u64)len << 56;
