@@ -283,17 +283,45 @@ def main():
     stats = eng.stats()
     map_sum, map_launches = eng.timings()         # k_map device ms, summed over the timed steps
     assert map_launches == args.steps, (map_launches, args.steps)
-    # every phase (events around each), on instrumented steps after the timed region
+    # every phase (events around each), on instrumented steps after the timed region; N > 1 also
+    # times the step's stages on the host clock with a synchronise after each (the shuffle through
+    # gloo, host-staged, has no engine events; RCCL's wcg_exchange / wcg_gather_merge have them)
     psteps = max(1, min(args.steps, 10))
     eng.enable_timing(2)
+    wall = {"map": 0.0, "shuffle": 0.0, "owner_reduce": 0.0, "gather_merge": 0.0}
+    map_stats = None
     for _ in range(psteps):
-        step()
+        if world == 1:
+            step()
+            continue
+        t0p = time.perf_counter()
+        eng.reset()
+        eng.map_device(dev.data_ptr(), n)
+        torch.cuda.synchronize()
+        t1p = time.perf_counter()
+        if map_stats is None:                     # this rank's map counters (the owners' jobs reset them)
+            map_stats = eng.stats()
+            t1p = time.perf_counter()
+        wd.shuffle(teng, args.nreduce)
+        torch.cuda.synchronize()
+        t2p = time.perf_counter()
+        teng.reduce()
+        torch.cuda.synchronize()
+        t3p = time.perf_counter()
+        wd.gather_merge(teng, fetch=False)
+        torch.cuda.synchronize()
+        t4p = time.perf_counter()
+        for k, a, b in (("map", t0p, t1p), ("shuffle", t1p, t2p), ("owner_reduce", t2p, t3p),
+                        ("gather_merge", t3p, t4p)):
+            wall[k] += (b - a) * 1e3
     ph_sum, _ = eng.timings()
     eng.enable_timing(0)
     if world > 1:                                 # every rank's counters and phase times
         per_rank = [None] * world
         dist.all_gather_object(per_rank, {"stats": stats, "phase_ms_avg":
-                                          {k: round(v / psteps, 4) for k, v in ph_sum.items()}})
+                                          {k: round(v / psteps, 4) for k, v in ph_sum.items()},
+                                          "phase_wall_ms_avg": {k: round(v / psteps, 4) for k, v in wall.items()},
+                                          "map_stats": map_stats})
 
     # ---- verify the last step's output against the oracle (outside the timed region)
     verified = None
@@ -379,6 +407,8 @@ def main():
             out["per_rank"] = per_rank
             out["phase_ms_avg_max_over_ranks"] = {
                 k: max(r["phase_ms_avg"][k] for r in per_rank) for k in per_rank[0]["phase_ms_avg"]}
+            out["phase_wall_ms_avg_max_over_ranks"] = {
+                k: max(r["phase_wall_ms_avg"][k] for r in per_rank) for k in per_rank[0]["phase_wall_ms_avg"]}
         out["verified_vs_oracle"] = verified
         if world == 1 and not args.no_end_to_end:
             out["end_to_end"] = end_to_end(eng, cfg, n)
