@@ -205,7 +205,80 @@ __device__ __forceinline__ u32 cont_mask4(u32 x) {
 #ifndef WCG_UTF8_GROUP
 #define WCG_UTF8_GROUP 8
 #endif
+#ifndef WCG_UTF8_COMPACT
+#define WCG_UTF8_COMPACT 1
+#endif
+// 4 bytes -> 4-bit mask of the possible lead bytes C2-F4 (SWAR: bit 7 set and low 7 bits in
+// 42-74; the additions cannot carry out of a byte)
+__device__ __forceinline__ u32 lead_mask4(u32 x) {
+    const u32 t = x & 0x7F7F7F7Fu;
+    const u32 c = (t + 0x3E3E3E3Eu) & ~(t + 0x0B0B0B0Bu) & x & 0x80808080u;
+    return (((c >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+__device__ __forceinline__ u32 utf8_mask_lds_all(uint4 c, u32 nx, LdsLetters lt);
+// Lead-compacted form (r03): only positions holding a lead byte (C2-F4) followed by a
+// continuation byte can start a multi-byte letter, and no two such positions are adjacent (the
+// byte after one is a continuation byte), so a chunk has at most 8 of them.  Eight slots decode
+// the chunk's such positions in turn (the lowest first; an empty slot decodes cp 0, not a letter)
+// instead of all 16 positions: C4 text averages 4.5 per non-ASCII chunk, and the decode's VALU is
+// what bounds k_map there.
 __device__ __forceinline__ u32 utf8_mask_lds(uint4 c, u32 nx, LdsLetters lt) {
+#if !WCG_UTF8_COMPACT
+    return utf8_mask_lds_all(c, nx, lt);
+#else
+    const u32 d0 = c.x, d1 = c.y, d2 = c.z, d3 = c.w, d4 = nx;
+    u32 m = (ascii_mask4(c.x & 0x7F7F7F7Fu) & ~high_mask4(c.x)) |
+            ((ascii_mask4(c.y & 0x7F7F7F7Fu) & ~high_mask4(c.y)) << 4) |
+            ((ascii_mask4(c.z & 0x7F7F7F7Fu) & ~high_mask4(c.z)) << 8) |
+            ((ascii_mask4(c.w & 0x7F7F7F7Fu) & ~high_mask4(c.w)) << 12);
+    const u32 cont = cont_mask4(c.x) | (cont_mask4(c.y) << 4) | (cont_mask4(c.z) << 8) |
+                     (cont_mask4(c.w) << 12) | (cont_mask4(nx) << 16);   // bit j: byte j
+    u32 L = (lead_mask4(c.x) | (lead_mask4(c.y) << 4) | (lead_mask4(c.z) << 8) | (lead_mask4(c.w) << 12)) &
+            (cont >> 1);
+    constexpr int NS = 8;
+    u32 cp[NS], span[NS];
+#pragma unroll
+    for (int g = 0; g < NS; g++) {
+        const bool has = L != 0u;
+        const u32 i = (u32)__builtin_ctz(L | 0x10000u) & 15u;
+        L &= L - 1u;
+        // dwords i >> 2 and (i >> 2) + 1 of the chunk (two levels of selects)
+        const bool s0 = (i & 4u) != 0, s1 = (i & 8u) != 0;
+        const u32 p0 = s0 ? d1 : d0, p1 = s0 ? d2 : d1, p2 = s0 ? d3 : d2, p3 = s0 ? d4 : d3;
+        const u32 wd = __builtin_amdgcn_alignbyte(s1 ? p3 : p1, s1 ? p2 : p0, i & 3u);
+        // as utf8_mask_lds_all, minus the lead test (b0 is C2-F4 in a filled slot)
+        const u32 b0 = wd & 0xFFu;
+        const u32 w = __builtin_clz(~(wd << 24));          // leading ones of b0: 2-4
+        const u32 need = (1u << ((w - 1) & 31)) - 1u;
+        const bool conts = ((cont >> (i + 1)) & need) == need;
+        const u32 x = ((b0 & (0x7Fu >> (w & 31))) << 18) | ((wd << 4) & 0x3F000u) | ((wd >> 10) & 0xFC0u) |
+                      ((wd >> 24) & 0x3Fu);
+        const u32 v = x >> ((24 - 6 * w) & 31);
+        const bool ok = has & conts & ((v >> ((5 * w - 4) & 31)) != 0u) & (v - 0xD800u >= 0x800u) &
+                        (v <= 0x10FFFFu);
+        cp[g] = ok ? v : 0u;
+        span[g] = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0, w & 31) << i;
+    }
+    u32 t[NS], bits[NS];
+#pragma unroll
+    for (int g = 0; g < NS; g++) {
+        const u32 b = cp[g] >> 8;
+        t[g] = lt.idx[b < LT_LDS_BLOCKS ? b : LT_LDS_BLOCKS];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < NS; g++) {
+        const u32 b = cp[g] >> 8;
+        bits[g] = lt.bits[(b < 8 ? b : t[g]) * 8 + ((cp[g] >> 5) & 7)];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < NS; g++) m |= ((bits[g] >> (cp[g] & 31)) & 1u) ? span[g] : 0u;
+    return m;
+#endif
+}
+// every position decoded (the form before r03's lead compaction; WCG_UTF8_COMPACT=0)
+__device__ __forceinline__ u32 utf8_mask_lds_all(uint4 c, u32 nx, LdsLetters lt) {
     const u32 d[5] = {c.x, c.y, c.z, c.w, nx};
     u32 m = (ascii_mask4(c.x & 0x7F7F7F7Fu) & ~high_mask4(c.x)) |
             ((ascii_mask4(c.y & 0x7F7F7F7Fu) & ~high_mask4(c.y)) << 4) |
