@@ -82,6 +82,101 @@ __device__ __forceinline__ void rb_local(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], 
         }
     }
 }
+#ifndef WCG_SORT_NET
+#define WCG_SORT_NET 1
+#endif
+// ---- the same network with every stage unrolled (r03): the compare distance is a constant, so
+//      the lane exchanges are single cross-lane moves (DPP quad_perm for 1 and 2, DPP row_ror:8
+//      for 8, ds_swizzle for 4 and 16, v_permlane32_swap for 32) instead of ds_bpermute with an
+//      address, and the compare-exchanges are selects instead of branches.  The position q is a
+//      payload only: equal prefixes may end in any order (the tie sort orders long keys; repeated
+//      inline keys are merged), so a pair compares (hi, lo) alone.  (The loop form ran ~48 VALU
+//      per entry and stage: C4's bucket sorts were 1.5 ms.)
+template <int D>
+__device__ __forceinline__ u32 lane_xor(u32 v) {
+    if constexpr (D == 1) return (u32)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+    else if constexpr (D == 2) return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+    else if constexpr (D == 4) return (u32)__builtin_amdgcn_ds_swizzle((int)v, (4 << 10) | 0x1F);
+    else if constexpr (D == 8) return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    else if constexpr (D == 16) return (u32)__builtin_amdgcn_ds_swizzle((int)v, (16 << 10) | 0x1F);
+    else {
+        static_assert(D == 32, "lane_xor: distance 1..32");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);   // r[0]: lanes 32-63 hold
+        return (threadIdx.x & 32) ? r[0] : r[1];                               // lanes 0-31 of v, r[1] vice versa
+    }
+}
+template <int D>
+__device__ __forceinline__ u64 lane_xor64(u64 v) {
+    return (u64)lane_xor<D>((u32)(v >> 32)) << 32 | lane_xor<D>((u32)v);
+}
+__device__ __forceinline__ bool hl_lt(u64 ah, u64 al, u64 bh, u64 bl) { return ah < bh || (ah == bh && al < bl); }
+// keep (p) if the pair's order asks for it: keep_min takes p when p < mine, the other side when
+// mine < p (both sides evaluate the same comparison, so a pair always swaps consistently)
+__device__ __forceinline__ void net_take(bool keep_min, u64& h, u64& l, u32& q, u64 ph, u64 pl, u32 pq) {
+    const bool take = keep_min ? hl_lt(ph, pl, h, l) : hl_lt(h, l, ph, pl);
+    h = take ? ph : h; l = take ? pl : l; q = take ? pq : q;
+}
+template <int NT, int E, u32 K, u32 J>
+__device__ __forceinline__ void net_stage(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
+    const u32 t = threadIdx.x;
+    if constexpr (J < (u32)E) {                   // both entries in this thread
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            if (e & J) continue;
+            const int f = e | (int)J;
+            const bool asc = (((u32)(t * E + e)) & K) == 0;
+            const bool sw = asc ? hl_lt(h[f], l[f], h[e], l[e]) : hl_lt(h[e], l[e], h[f], l[f]);
+            const u64 eh = h[e], el = l[e]; const u32 eq = q[e];
+            h[e] = sw ? h[f] : eh; l[e] = sw ? l[f] : el; q[e] = sw ? q[f] : eq;
+            h[f] = sw ? eh : h[f]; l[f] = sw ? el : l[f]; q[f] = sw ? eq : q[f];
+        }
+    } else {
+        // J >= E: the pair's direction depends on the thread only
+        const u32 i0 = t * E;
+        const bool keep_min = ((i0 & J) == 0) == ((i0 & K) == 0);
+        if constexpr (J < 64u * E) {
+            constexpr int D = (int)(J / E);
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const u64 ph = lane_xor64<D>(h[e]), pl = lane_xor64<D>(l[e]);
+                const u32 pq = lane_xor<D>(q[e]);
+                net_take(keep_min, h[e], l[e], q[e], ph, pl, pq);
+            }
+        } else {
+            __syncthreads();                      // the previous LDS stage's readers are done
+#pragma unroll
+            for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = h[e]; kl[i] = l[e]; kp[i] = (uint16_t)q[e]; }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const u32 i = (t * E + e) ^ J;
+                net_take(keep_min, h[e], l[e], q[e], kh[i], kl[i], kp[i]);
+            }
+        }
+    }
+}
+template <int NT, int E, u32 K, u32 J>
+__device__ __forceinline__ void net_stages_j(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
+    net_stage<NT, E, K, J>(h, l, q, kh, kl, kp);
+    if constexpr (J > 1) net_stages_j<NT, E, K, J / 2>(h, l, q, kh, kl, kp);
+}
+template <int NT, int E, u32 K>
+__device__ __forceinline__ void net_stages_k(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
+    net_stages_j<NT, E, K, K / 2>(h, l, q, kh, kl, kp);
+    if constexpr (K < (u32)NT * E) net_stages_k<NT, E, K * 2>(h, l, q, kh, kl, kp);
+}
+
+template <int NT, int E>
+__device__ __forceinline__ void reg_bitonic_unrolled(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
+    const u32 t = threadIdx.x;
+    net_stages_k<NT, E, 2>(h, l, q, kh, kl, kp);
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = h[e]; kl[i] = l[e]; kp[i] = (uint16_t)q[e]; }
+    __syncthreads();
+}
+
+// the loop form: (hi, lo, position) order
 template <int NT, int E>
 __device__ __forceinline__ void reg_bitonic(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
     constexpr u32 P = NT * E;
@@ -730,13 +825,19 @@ template <int E>
 __device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* kl, uint16_t* kp) {
     u64 h[E], l[E];
     u32 q[E];
+    bool maxkey = false;
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const u32 i = threadIdx.x * E + e;
         if (i < m) { h[e] = X[i].hi; l[e] = X[i].lo; } else { h[e] = ~0ull; l[e] = ~0ull; }
         q[e] = i;
+        maxkey |= i < m && (h[e] & l[e]) == ~0ull;
     }
-    reg_bitonic<SB_NT, E>(h, l, q, kh, kl, kp);
+    // The unrolled network orders (hi, lo) only, so the padding (all ones) must compare above
+    // every record: a record whose prefix is all ones (no key the map produces: byte 15 is 0 or a
+    // letter byte - only a crafted import or run) takes the (hi, lo, position) network.
+    if (WCG_SORT_NET && !__syncthreads_or(maxkey)) reg_bitonic_unrolled<SB_NT, E>(h, l, q, kh, kl, kp);
+    else reg_bitonic<SB_NT, E>(h, l, q, kh, kl, kp);
 }
 
 // one workgroup per bucket: bitonic sort of (hi, lo, position) in registers (LDS for the widest
