@@ -85,6 +85,12 @@ __device__ __forceinline__ void rb_local(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], 
 #ifndef WCG_SORT_NET
 #define WCG_SORT_NET 1
 #endif
+#ifndef WCG_SORT_NET_BIG
+#define WCG_SORT_NET_BIG 0     // 1: the 8-entry networks (buckets of 1025-2048 records) unrolled too (177 VGPRs: measured no faster)
+#endif
+#ifndef WCG_SORT_NET_FENCE
+#define WCG_SORT_NET_FENCE 1
+#endif
 // ---- the same network with every stage unrolled (r03): the compare distance is a constant, so
 //      the lane exchanges are single cross-lane moves (DPP quad_perm for 1 and 2, DPP row_ror:8
 //      for 8, ds_swizzle for 4 and 16, v_permlane32_swap for 32) instead of ds_bpermute with an
@@ -112,8 +118,14 @@ __device__ __forceinline__ u64 lane_xor64(u64 v) {
 __device__ __forceinline__ bool hl_lt(u64 ah, u64 al, u64 bh, u64 bl) { return ah < bh || (ah == bh && al < bl); }
 // keep (p) if the pair's order asks for it: keep_min takes p when p < mine, the other side when
 // mine < p (both sides evaluate the same comparison, so a pair always swaps consistently)
+// (x < y when dir, y < x otherwise, as lane-mask logic: a select between two comparisons was
+// materialised through VGPRs)
+__device__ __forceinline__ bool hl_dir_lt(bool dir, u64 xh, u64 xl, u64 yh, u64 yl) {
+    const bool heq = xh == yh, lt = (xh < yh) | (heq & (xl < yl)), eq = heq & (xl == yl);
+    return (dir & lt) | (!dir & !lt & !eq);
+}
 __device__ __forceinline__ void net_take(bool keep_min, u64& h, u64& l, u32& q, u64 ph, u64 pl, u32 pq) {
-    const bool take = keep_min ? hl_lt(ph, pl, h, l) : hl_lt(h, l, ph, pl);
+    const bool take = hl_dir_lt(keep_min, ph, pl, h, l);
     h = take ? ph : h; l = take ? pl : l; q = take ? pq : q;
 }
 template <int NT, int E, u32 K, u32 J>
@@ -125,7 +137,7 @@ __device__ __forceinline__ void net_stage(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E],
             if (e & J) continue;
             const int f = e | (int)J;
             const bool asc = (((u32)(t * E + e)) & K) == 0;
-            const bool sw = asc ? hl_lt(h[f], l[f], h[e], l[e]) : hl_lt(h[e], l[e], h[f], l[f]);
+            const bool sw = hl_dir_lt(asc, h[f], l[f], h[e], l[e]);
             const u64 eh = h[e], el = l[e]; const u32 eq = q[e];
             h[e] = sw ? h[f] : eh; l[e] = sw ? l[f] : el; q[e] = sw ? q[f] : eq;
             h[f] = sw ? eh : h[f]; l[f] = sw ? el : l[f]; q[f] = sw ? eq : q[f];
@@ -158,6 +170,9 @@ __device__ __forceinline__ void net_stage(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E],
 template <int NT, int E, u32 K, u32 J>
 __device__ __forceinline__ void net_stages_j(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
     net_stage<NT, E, K, J>(h, l, q, kh, kl, kp);
+#if WCG_SORT_NET_FENCE
+    __builtin_amdgcn_sched_barrier(0);            // stages stay apart (register pressure)
+#endif
     if constexpr (J > 1) net_stages_j<NT, E, K, J / 2>(h, l, q, kh, kl, kp);
 }
 template <int NT, int E, u32 K>
@@ -836,7 +851,8 @@ __device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* 
     // The unrolled network orders (hi, lo) only, so the padding (all ones) must compare above
     // every record: a record whose prefix is all ones (no key the map produces: byte 15 is 0 or a
     // letter byte - only a crafted import or run) takes the (hi, lo, position) network.
-    if (WCG_SORT_NET && !__syncthreads_or(maxkey)) reg_bitonic_unrolled<SB_NT, E>(h, l, q, kh, kl, kp);
+    if (WCG_SORT_NET && (E < 8 || WCG_SORT_NET_BIG) && !__syncthreads_or(maxkey))
+        reg_bitonic_unrolled<SB_NT, E>(h, l, q, kh, kl, kp);
     else reg_bitonic<SB_NT, E>(h, l, q, kh, kl, kp);
 }
 
