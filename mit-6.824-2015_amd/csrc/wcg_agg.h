@@ -401,6 +401,9 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
 #ifndef WCG_RP_QB
 #define WCG_RP_QB 48
 #endif
+#ifndef WCG_RP_PREFETCH
+#define WCG_RP_PREFETCH 0
+#endif
 constexpr u32 RP_QB = WCG_RP_QB;       // LDS units per sub-bucket buffer (48 KiB in all: two k_rp
                                        // workgroups per CU; 96 measured 6% slower on C4)
 struct RpArgs {
@@ -410,7 +413,10 @@ struct RpArgs {
     u64* pool2; u64 cap2; u32* region_len2;                    // sub-bucket regions (pass 2's input)
     GEntry* gtab; u64 gmask; DevState* st;
 };
-__global__ __launch_bounds__(AGG_NT) void k_rp(RpArgs a) {
+#ifndef WCG_RP_MINB
+#define WCG_RP_MINB 1
+#endif
+__global__ __launch_bounds__(AGG_NT, WCG_RP_MINB) void k_rp(RpArgs a) {
     __shared__ u64 sbuf[AGG_Q][RP_QB];
     __shared__ u32 scnt[AGG_Q], sfill[AGG_Q], gpos[AGG_Q], gbase[AGG_Q];
     __shared__ u32 sdirect[AGG_Q];            // 1: this round's buffer goes out entry by entry
@@ -454,6 +460,31 @@ __global__ __launch_bounds__(AGG_NT) void k_rp(RpArgs a) {
         my_global++;
         ginsert(gtab, gmask, k0, k1, gslot(key_hash(k0, k1)), c, st);
     };
+#if WCG_RP_PREFETCH
+    // batches in (region, offset) order; the next batch's units are loaded before this one is
+    // split, so their latency overlaps the LDS work, the barriers and the stores
+    u32 k = k0_, base = 0, n = k < k1_ ? a.region_len[(u64)k * a.P + p] : 0u;
+    while (k < k1_ && n == 0) { k++; n = k < k1_ ? a.region_len[(u64)k * a.P + p] : 0u; }
+    u64 nu[6];
+    auto load6 = [&](u32 kk, u32 bb, u32 nn, u64 (&x)[6]) {
+        const u64* s = a.pool + ((u64)kk * a.P + p) * a.region_cap;
+        const u32 i = bb + 4 * tid;
+#pragma unroll
+        for (int j = 0; j < 6; j++) x[j] = kk < k1_ && i + j < nn ? s[i + j] : 0;
+    };
+    load6(k, 0, n, nu);
+    while (k < k1_) {
+        u64 u[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) u[j] = nu[j];
+        u32 kn = k, bn = base + AGG_BATCH, nn = n;
+        if (bn >= n) {
+            bn = 0;
+            do { kn++; nn = kn < k1_ ? a.region_len[(u64)kn * a.P + p] : 0u; } while (kn < k1_ && nn == 0);
+        }
+        load6(kn, bn, nn, nu);
+        {
+#else
     for (u32 k = k0_; k < k1_; k++) {
     const u64 reg = (u64)k * a.P + p;
     const u32 n = a.region_len[reg];
@@ -463,6 +494,7 @@ __global__ __launch_bounds__(AGG_NT) void k_rp(RpArgs a) {
         u64 u[6];
 #pragma unroll
         for (int j = 0; j < 6; j++) u[j] = i0 + j < n ? src[i0 + j] : 0;
+#endif
         u64 k0[4], k1[4], c[4];
         bool v[4];
         u32 nu[4];
@@ -512,6 +544,9 @@ __global__ __launch_bounds__(AGG_NT) void k_rp(RpArgs a) {
         for (u32 q = tid; q < AGG_Q; q += AGG_NT) { scnt[q] = 0; sfill[q] = 0; }
         __syncthreads();
     }
+#if WCG_RP_PREFETCH
+        k = kn; base = bn; n = nn;
+#endif
     }
     for (u32 q = tid; q < AGG_Q; q += AGG_NT) a.region_len2[(u64)b * AGG_Q + q] = gpos[q] < cap2 ? gpos[q] : (u32)cap2;
     for (int d = 32; d >= 1; d >>= 1) my_global += __shfl_xor(my_global, d, 64);

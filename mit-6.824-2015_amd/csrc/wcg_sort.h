@@ -500,9 +500,13 @@ constexpr u32 SS_TOP = 1024;           // top-level splitters staged in LDS abov
 constexpr u32 SB_CAP = 2048;           // bucket records sorted in LDS (18 B each: 36 KiB)
 constexpr int SB_NT = 256;             // bucket sort workgroups
 #ifndef WCG_SS_U
-#define WCG_SS_U 4
+#define WCG_SS_U 2
 #endif
-constexpr int SS_U = WCG_SS_U;         // records per thread in flight (hist / scatter)
+constexpr int SS_U = WCG_SS_U;         // records per thread in flight (hist / scatter; r03: 2 - 4 and 1
+                                       // measured 40-70 us slower on C4's 2.4e7-record sort)
+#ifndef WCG_SS_ABL
+#define WCG_SS_ABL 0                   // diagnostics: 1 = k_ss_hist skips its global search levels (wrong order)
+#endif
 
 struct SortArgs {
     const Rec* rec;          // compacted records (index = position)
@@ -645,7 +649,7 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) 
                 l[k] = tl > 0 ? ss_top_index(a, tl - 1) + 1 : 0;
                 m[k] = (tl < SS_TOP ? ss_top_index(a, tl) : a.B - 1) - l[k];
             }
-            while (true) {                            // lower bounds in [l, l + m), interleaved
+            while (!WCG_SS_ABL) {                     // lower bounds in [l, l + m), interleaved
                 bool any = false;
                 u64 sh[SS_U];
 #pragma unroll
