@@ -557,10 +557,25 @@ __global__ void k_ss_split(SortArgs a) {
     a.sph[b] = s.hi; a.spl[b] = s.lo; a.spi[b] = (u32)s.cnt;
 }
 
+// The logical workgroup of a hist / scatter block (its record range and histogram column).
+// Within a bucket the scatter writes workgroup 0's records, then workgroup 1's, ...: a bucket's
+// 128-byte lines are shared by neighbouring workgroups, and blocks are dispatched to the 8 XCDs
+// round-robin, so with the identity mapping every shared line was written from up to four XCDs'
+// L2s (partial-line write-backs).  Consecutive logical workgroups run on one XCD instead.
+#ifndef WCG_SS_XCD
+#define WCG_SS_XCD 1
+#endif
+__device__ __forceinline__ u32 ss_wg(const SortArgs& a) {
+    const u32 b = blockIdx.x;
+    if (!WCG_SS_XCD || (a.G & 7u)) return b;
+    return (b & 7u) * (a.G >> 3) + (b >> 3);
+}
+
 __device__ __forceinline__ void ss_range(const SortArgs& a, u64& i0, u64& i1) {
     const u64 n = ss_count(a);
-    i0 = n * blockIdx.x / a.G;
-    i1 = n * (blockIdx.x + 1) / a.G;
+    const u32 g = ss_wg(a);
+    i0 = n * g / a.G;
+    i1 = n * (g + 1) / a.G;
 }
 
 // Up to SS_LDSB buckets every splitter is staged in LDS (a binary search of LDS reads), and the
@@ -674,7 +689,7 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) 
             }
         }
         __syncthreads();
-        for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + blockIdx.x] = h[b];
+        for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + ss_wg(a)] = h[b];
         return;
     }
     for (u64 i = i0 + threadIdx.x; i < i1; i += NT) {
@@ -685,7 +700,7 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) 
         atomicAdd(&h[b], 1u);
     }
     __syncthreads();
-    for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + blockIdx.x] = h[b];
+    for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + ss_wg(a)] = h[b];
 }
 
 // the sample of a small sort (S <= TS_TILE) by ranks: rank = the samples below it in the
@@ -723,7 +738,7 @@ template <bool SMALL>
 __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_scatter(SortArgs a) {
     constexpr int NT = SMALL ? SS_NT : SSL_NT;
     __shared__ u32 cur[SMALL ? SS_LDSB : SS_MAXB];
-    for (u32 b = threadIdx.x; b < a.B; b += NT) cur[b] = a.hist[(u64)b * a.G + blockIdx.x];
+    for (u32 b = threadIdx.x; b < a.B; b += NT) cur[b] = a.hist[(u64)b * a.G + ss_wg(a)];
     __syncthreads();
     u64 i0, i1;
     ss_range(a, i0, i1);
