@@ -456,9 +456,12 @@ int sort_records(wcg_ctx* c) {
     // dependent reads); the large-B kernels keep one 128 KiB histogram per CU
     a.G = (u32)std::max<u64>(1, std::min<u64>(cdiv(np, small ? 1024 : 4096), (u64)c->ncu * (small ? 4 : 1)));
     RC(ensure(c, &c->bid, &c->bid_cap, n));
-    RC(ensure(c, &c->hist, &c->hist_cap, (u64)a.B * a.G));
+    // large B: a workgroup-major histogram and the bucket starts after it (B + 1 entries)
+    const bool tr = !small && WCG_SS_TR;
+    RC(ensure(c, &c->hist, &c->hist_cap, (u64)a.B * a.G + (tr ? a.B + 1 : 0)));
     RC(ensure(c, &c->irec, &c->irec_cap, 2 * n));
     a.bid = c->bid; a.hist = c->hist;
+    a.bstart = tr ? c->hist + (u64)a.B * a.G : nullptr;
     a.irec = c->irec; a.irec2 = c->irec + n;
     a.sph = a.spl = nullptr; a.spi = nullptr;
     if (!small) {                                  // the splitters as arrays (hi, lo, index)
@@ -469,7 +472,12 @@ int sort_records(wcg_ctx* c) {
     if (small) k_ss_hist<true><<<a.G, SS_NT, 0, c->stream>>>(a);
     else k_ss_hist<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
-    RC(scan_u32(c, c->hist, (u64)a.B * a.G));
+    if (tr) {
+        k_ss_colscan<<<cdiv(a.B, 256), 256, 0, c->stream>>>(a.hist, a.B, a.G, a.bstart);
+        RC(scan_u32(c, a.bstart, a.B));
+    } else {
+        RC(scan_u32(c, c->hist, (u64)a.B * a.G));
+    }
     if (small) k_ss_scatter<true><<<a.G, SS_NT, 0, c->stream>>>(a);
     else k_ss_scatter<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
     k_ss_bucket<false><<<a.B, SB_NT, 0, c->stream>>>(a);

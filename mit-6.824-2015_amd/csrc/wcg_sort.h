@@ -502,6 +502,9 @@ constexpr int SB_NT = 256;             // bucket sort workgroups
 #ifndef WCG_SS_U
 #define WCG_SS_U 2
 #endif
+#ifndef WCG_SS_TR
+#define WCG_SS_TR 1                    // large B: workgroup-major histogram + k_ss_colscan
+#endif
 constexpr int SS_U = WCG_SS_U;         // records per thread in flight (hist / scatter; r03: 2 - 4 and 1
                                        // measured 40-70 us slower on C4's 2.4e7-record sort)
 #ifndef WCG_SS_ABL
@@ -526,6 +529,8 @@ struct SortArgs {
     u64* nkeys;              // distinct keys (dedupe)
     u64* sph; u64* spl; u32* spi;   // splitters 0..B-2 as arrays (hi, lo, record index): the
                                     // searches' global reads stay within 20 B per splitter (L2)
+    u32* bstart;             // large B (SS_TR): hist is workgroup-major [G][B] and bstart[b] the
+                             // start of bucket b (k_ss_colscan); null: hist is [B][G]
 };
 
 // the records to sort: a.n, or the count the device holds (a plan made for another count only
@@ -689,7 +694,12 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) 
             }
         }
         __syncthreads();
-        for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + ss_wg(a)] = h[b];
+        if (a.bstart) {                          // one contiguous row per workgroup
+            u32* row = a.hist + (u64)ss_wg(a) * a.B;
+            for (u32 b = threadIdx.x; b < a.B; b += NT) row[b] = h[b];
+        } else {
+            for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + ss_wg(a)] = h[b];
+        }
         return;
     }
     for (u64 i = i0 + threadIdx.x; i < i1; i += NT) {
@@ -738,7 +748,12 @@ template <bool SMALL>
 __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_scatter(SortArgs a) {
     constexpr int NT = SMALL ? SS_NT : SSL_NT;
     __shared__ u32 cur[SMALL ? SS_LDSB : SS_MAXB];
-    for (u32 b = threadIdx.x; b < a.B; b += NT) cur[b] = a.hist[(u64)b * a.G + ss_wg(a)];
+    if (!SMALL && a.bstart) {
+        const u32* row = a.hist + (u64)ss_wg(a) * a.B;
+        for (u32 b = threadIdx.x; b < a.B; b += NT) cur[b] = a.bstart[b] + row[b];
+    } else {
+        for (u32 b = threadIdx.x; b < a.B; b += NT) cur[b] = a.hist[(u64)b * a.G + ss_wg(a)];
+    }
     __syncthreads();
     u64 i0, i1;
     ss_range(a, i0, i1);
@@ -758,6 +773,29 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_scatter(SortArgs 
         for (int k = 0; k < SS_U; k++)
             if (i + (u64)k * NT < i1) a.irec[d[k]] = r[k];
     }
+}
+
+// Workgroup-major histogram (large B): per bucket b, the exclusive prefix over workgroups in place
+// and the bucket's total in bstart[b] (then scanned into the starts).  Threads take consecutive
+// buckets, so every read and write is coalesced.  ([B][G] written by the histogram kernel was a
+// column per workgroup: 32768 scattered 4-byte writes per workgroup, and as many scattered reads
+// in the scatter.)
+__global__ void k_ss_colscan(u32* hist, u32 B, u32 G, u32* bstart) {
+    const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    u32 run = 0;
+    constexpr u32 CS_U = 32;                  // loads in flight per thread (G <= ncu: a few rounds)
+    for (u32 g0 = 0; g0 < G; g0 += CS_U) {
+        u32 v[CS_U];
+#pragma unroll
+        for (u32 k = 0; k < CS_U; k++) v[k] = g0 + k < G ? hist[(u64)(g0 + k) * B + b] : 0u;
+#pragma unroll
+        for (u32 k = 0; k < CS_U; k++) {
+            if (g0 + k < G) hist[(u64)(g0 + k) * B + b] = run;
+            run += v[k];
+        }
+    }
+    bstart[b] = run;
 }
 
 // Repeated inline keys (the record log of k_agg's pass 2 and the compacted tables may hold one
@@ -885,8 +923,8 @@ __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
     __shared__ u64 kh[CAP], kl[CAP];               // workgroups per CU (the register limit)
     __shared__ uint16_t kp[CAP];
     const u32 b = blockIdx.x;
-    const u64 s = a.hist[(u64)b * a.G];
-    const u64 e = b + 1 < a.B ? a.hist[(u64)(b + 1) * a.G] : ss_count(a);
+    const u64 s = a.bstart ? a.bstart[b] : a.hist[(u64)b * a.G];
+    const u64 e = b + 1 < a.B ? (a.bstart ? a.bstart[b + 1] : a.hist[(u64)(b + 1) * a.G]) : ss_count(a);
     const u64 m = e - s;
     if (m == 0 || (m > 4 * SB_NT) != BIG) return;
     if (m > SB_CAP) { ss_global_sort(a, s, m, kh, kl, kp); return; }
