@@ -505,6 +505,10 @@ constexpr int SB_NT = 256;             // bucket sort workgroups
 #ifndef WCG_SS_TR
 #define WCG_SS_TR 1                    // large B: workgroup-major histogram + k_ss_colscan
 #endif
+#ifndef WCG_SS_UX
+#define WCG_SS_UX 2                    // the scatter's records per thread in flight (C4: 2 1.05 ms, 4 1.06, 8 1.09)
+#endif
+constexpr int SS_UX = WCG_SS_UX;
 constexpr int SS_U = WCG_SS_U;         // records per thread in flight (hist / scatter; r03: 2 - 4 and 1
                                        // measured 40-70 us slower on C4's 2.4e7-record sort)
 #ifndef WCG_SS_ABL
@@ -757,20 +761,20 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_scatter(SortArgs 
     __syncthreads();
     u64 i0, i1;
     ss_range(a, i0, i1);
-    // SS_U records per thread at a time: their loads, cursor atomics and stores issue together
-    for (u64 i = i0 + threadIdx.x; i < i1; i += (u64)NT * SS_U) {
-        u32 b[SS_U], d[SS_U];
-        Rec r[SS_U];
+    // SS_UX records per thread at a time: their loads, cursor atomics and stores issue together
+    for (u64 i = i0 + threadIdx.x; i < i1; i += (u64)NT * SS_UX) {
+        u32 b[SS_UX], d[SS_UX];
+        Rec r[SS_UX];
 #pragma unroll
-        for (int k = 0; k < SS_U; k++) {
+        for (int k = 0; k < SS_UX; k++) {
             const u64 j = i + (u64)k * NT;
             if (j < i1) { b[k] = a.bid[j]; r[k] = a.rec[j]; }
         }
 #pragma unroll
-        for (int k = 0; k < SS_U; k++)
+        for (int k = 0; k < SS_UX; k++)
             if (i + (u64)k * NT < i1) d[k] = atomicAdd(&cur[b[k]], 1u);
 #pragma unroll
-        for (int k = 0; k < SS_U; k++)
+        for (int k = 0; k < SS_UX; k++)
             if (i + (u64)k * NT < i1) a.irec[d[k]] = r[k];
     }
 }
