@@ -434,7 +434,10 @@ int sort_records(wcg_ctx* c) {
     // bucket past 4 * SB_NT records takes the 8-entry register network (twice the work per record)
     // bucket past 4 * SB_NT records takes the 8-entry register network (twice the work per record);
     // small sorts keep the sample within one workgroup's sort (TS_TILE) when 4+ per bucket allow
-    u64 ovs = a.B > SS_LDSB ? 2 * SS_OVS : SS_OVS;
+#ifndef WCG_SS_OVS_L
+#define WCG_SS_OVS_L 2
+#endif
+    u64 ovs = a.B > SS_LDSB ? WCG_SS_OVS_L * SS_OVS : SS_OVS;
     if (a.B <= SS_LDSB && a.B * ovs > TS_TILE && a.B * 4 <= TS_TILE) ovs = TS_TILE / a.B;
     a.S = a.B > 1 ? std::min<u64>(np, (u64)a.B * ovs) : 0;
     a.smp = nullptr;
