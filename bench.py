@@ -11,7 +11,8 @@ After the timed steps the merged file is checked byte for byte against the C ora
 against the sum of every rank's oracle counts); a mismatch exits 3 without printing a rate.
 
   python bench.py --gpus N --steps K --warmup W
-N > 1 is launched by torch.distributed.run (one rank per GPU, backend nccl = RCCL).
+N > 1: one rank per GPU (backend nccl = RCCL).  Started by an external torch.distributed.run, or,
+when WORLD_SIZE is not set, by this script itself (wcg/launch.py) before any GPU call.
 """
 from __future__ import annotations
 
@@ -49,6 +50,8 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N > 1 path with host-staged records, ranks may share a GPU")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="--gpus N > 1 without an external launcher: seconds before the rank processes are stopped")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per map launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -191,6 +194,12 @@ def end_to_end(eng, cfg, n, reps=3):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # a plain `python bench.py --gpus N`: start the N rank processes here (one per GPU, under
+        # torch.distributed.run) and relay rank 0's line.  This process never initialises a GPU;
+        # a failed rank or a job past --launch-timeout ends the run with a non-zero status.
+        from wcg.launch import launch_ranks
+        sys.exit(launch_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus, args.launch_timeout))
     import torch
     import torch.distributed as dist
     import wcg
@@ -200,9 +209,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world == 1 and args.gpus > 1:
-        print("bench.py: N>1 must be launched with torch.distributed.run", file=sys.stderr)
-        sys.exit(2)
     gloo = args.dist_backend == "gloo"
     if gloo:                                  # rehearsal: ranks may share the box's GPU(s)
         local = local % torch.cuda.device_count()
@@ -269,13 +275,18 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # every step ends in a host wait (wcg_reduce reads back the formatted size; the N > 1 Merge is
+    # synchronous at root), so the host clock between steps times each step without extra work
     t0 = time.perf_counter()
+    marks = [t0]
     for _ in range(args.steps):
         step()
+        marks.append(time.perf_counter())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    step_ms = [(b - a) * 1e3 for a, b in zip(marks, marks[1:])]
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if gloo else "cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -318,7 +329,7 @@ def main():
     eng.enable_timing(0)
     if world > 1:                                 # every rank's counters and phase times
         per_rank = [None] * world
-        dist.all_gather_object(per_rank, {"stats": stats, "phase_ms_avg":
+        dist.all_gather_object(per_rank, {"stats": stats, "step_ms": step_ms, "phase_ms_avg":
                                           {k: round(v / psteps, 4) for k, v in ph_sum.items()},
                                           "phase_wall_ms_avg": {k: round(v / psteps, 4) for k, v in wall.items()},
                                           "map_stats": map_stats})
@@ -393,6 +404,19 @@ def main():
                          "traffic": traffic, "avg_launch_ms": round(avg_map_ms, 4),
                          "algorithmic_bytes_per_launch": n},
         }
+        # per-step spread (host clock between steps; N > 1: each step's slowest rank)
+        if world > 1:
+            srt = sorted(max(v) for v in zip(*[r["step_ms"] for r in per_rank]))
+        else:
+            srt = sorted(step_ms)
+
+        def q(f):
+            return round(srt[min(len(srt) - 1, int(f * (len(srt) - 1) + 0.5))], 4)
+        out["ms_per_step_median"] = q(0.5)
+        out["ms_per_step_spread"] = {"min": q(0.0), "p10": q(0.1), "p90": q(0.9), "max": q(1.0),
+                                     "how": "host clock between steps (each step ends in a host wait); "
+                                            "value uses the mean over the bracketed loop"}
+        out["value_at_median_step"] = round(all_bytes / (q(0.5) * 1e-3) / 1e9, 3)
         out["stats"] = stats
         out["phase_ms_avg"] = {k: round(v / psteps, 4) for k, v in ph_sum.items()
                                if world > 1 or k in ("map", "agg", "compact", "sort", "format")}

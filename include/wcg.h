@@ -166,22 +166,50 @@ WCG_API int wcg_export_write(wcg_ctx *ctx, void *dev_dst);
  *                    config-5 master RPC, torch.distributed, a file - 128 opaque bytes)
  *   wcg_comm_init    ncclCommInitRank for this context (world may be 1)
  *   wcg_exchange     export the local aggregate by owner = (ihash % nreduce) % world into a send
- *                    buffer, ncclAllToAll the unit counts, ONE host read of them, grouped
- *                    ncclSend/ncclRecv of the 32-byte units, then this context keeps exactly the
- *                    keys of the partitions it owns (tables cleared, received units imported).
- *                    All device work is ordered on the context's stream; *sent / *received =
- *                    units (may be NULL).  Follow with wcg_reduce (DoReduce of the owned
- *                    partitions: sorted "key: count" run of this rank).
+ *                    buffer, ncclAllGather every rank's row {status, buffer capacities, units per
+ *                    owner}, ONE host read of that world x world matrix, the plan of
+ *                    wcg_exchange_plan, grouped ncclSend/ncclRecv of the 32-byte units, then this
+ *                    context keeps exactly the keys of the partitions it owns (tables cleared,
+ *                    received units imported).  All device work is ordered on the context's
+ *                    stream; *sent / *received = units (may be NULL).  Follow with wcg_reduce
+ *                    (DoReduce of the owned partitions: sorted "key: count" run of this rank).
  *   wcg_gather_merge after wcg_reduce on every rank: every rank's sorted run goes to `root`
- *                    (ncclAllGather of the run sizes, one host read, ncclSend/ncclRecv), which
- *                    merges the runs on its GPU (as wcg_merge_runs) into its result.  On root
- *                    *nkeys / *nbytes describe the merged file; elsewhere they are 0.
- * Collective calls: every rank of the communicator makes them in the same order. */
+ *                    (ncclAllGather of {status, run size, capacity}, one host read,
+ *                    ncclSend/ncclRecv, placement of wcg_gather_plan), which merges the runs on
+ *                    its GPU (as wcg_merge_runs) into its result.  On root *nkeys / *nbytes
+ *                    describe the merged file; elsewhere they are 0.
+ * Collective calls: every rank of the communicator makes them in the same order.  A rank that
+ * fails before data moves (a full table: WCG_EFULL; a call out of order; an allocation) still
+ * joins the collectives with its status, and then EVERY rank returns an error (no rank is left
+ * waiting in a send or receive); no units have moved and the tables are as they were. */
 #define WCG_COMM_ID_BYTES 128
 WCG_API int wcg_comm_id(uint8_t *id_out /* WCG_COMM_ID_BYTES */);
 WCG_API int wcg_comm_init(wcg_ctx *ctx, const uint8_t *id /* WCG_COMM_ID_BYTES */, int rank, int world);
 WCG_API int wcg_exchange(wcg_ctx *ctx, uint32_t nreduce, uint64_t *sent, uint64_t *received);
 WCG_API int wcg_gather_merge(wcg_ctx *ctx, int root, uint64_t *nkeys, uint64_t *nbytes);
+
+/* The host-side plan of the shuffle and of Merge's gather (pure arithmetic, no device; what
+ * wcg_exchange / wcg_gather_merge compute from the gathered counts).
+ *   wcg_exchange_plan: counts[s * world + d] = units rank s sends to rank d.  For `rank`:
+ *     send_off[d] / send_cnt[d] = where its units for d start in its send buffer and how many;
+ *     recv_off[s] / recv_cnt[s] = where the units from s land in its receive buffer (source-rank
+ *     order); totals[2] = {units sent, units received}.  Output arrays may be NULL.
+ *   wcg_gather_plan: sizes[p] = bytes of rank p's sorted run; run_off[p] = where it lands in
+ *     root's receive buffer (root's own run is copied to run_off[root]); *total = all bytes. */
+WCG_API int wcg_exchange_plan(const uint64_t *counts, uint32_t world, uint32_t rank, uint64_t *send_off,
+                              uint64_t *send_cnt, uint64_t *recv_off, uint64_t *recv_cnt, uint64_t *totals);
+WCG_API int wcg_gather_plan(const uint64_t *sizes, uint32_t world, uint32_t root, uint64_t *run_off,
+                            uint64_t *total);
+
+/* The same shuffle and Merge across `world` contexts of ONE process (e.g. several contexts on one
+ * GPU standing in for the ranks of a node): the count matrix, the plans above, the export, import
+ * and merge kernels are wcg_exchange's and wcg_gather_merge's; device-to-device copies stand in
+ * for the RCCL sends and receives.  sent[world] / received[world] get each context's units. A
+ * test transport for world > 1 where one GPU cannot host several RCCL ranks. Synchronous. */
+WCG_API int wcg_exchange_local(wcg_ctx **ctxs, uint32_t world, uint32_t nreduce, uint64_t *sent,
+                               uint64_t *received);
+WCG_API int wcg_gather_merge_local(wcg_ctx **ctxs, uint32_t world, uint32_t root, uint64_t *nkeys,
+                                   uint64_t *nbytes);
 
 /* Merge (mapreduce.go:284-321) of sorted runs: dev_text holds nruns formatted outputs back to
  * back (each a sorted "key: count\n" file, e.g. the wcg_reduce output of every owner rank, with

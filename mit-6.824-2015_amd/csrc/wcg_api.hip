@@ -65,6 +65,10 @@ struct wcg_ctx {
     // read-back, and the sort is planned for the previous job's count (nrec_hint)
     bool dev_sized = false;
     u64 nrec_hint = 0;
+    // DevState's nrec / nlong are zero on the device: wcg_reset cleared them, or a one-pass
+    // k_agg did, and no compaction has counted into them since (a second wcg_reduce
+    // without a map in between would otherwise append to the first one's count)
+    bool counts_clean = false;
     Rec* irec = nullptr; u64 irec_cap = 0;
     LEnt* lent = nullptr; u64 lent_cap = 0;   // long-key partitions: LQ x lpart_cap entries
     u64* spill = nullptr; u64 spill_cap = 0;  // k_agg pass-1 spill regions
@@ -103,8 +107,9 @@ struct wcg_ctx {
     // RCCL shuffle (wcg_comm_init / wcg_exchange / wcg_gather_merge)
     ncclComm_t comm = nullptr;
     int comm_rank = 0, comm_world = 0;
-    u64* d_xcnt = nullptr;                    // [4 * EX_MAX_RANKS]: received unit counts, run sizes
-    u64* h_xcnt = nullptr;                    // pinned [4 * EX_MAX_RANKS]
+    u32 x_world = 0;                          // the exchange buffers are sized for this world
+    u64* d_xrow = nullptr;                    // this rank's row, the status word, the gathered matrix
+    u64* h_x = nullptr;                       // pinned: row header, status, send offsets, matrix
     Rec* xrecv = nullptr; u64 xrecv_cap = 0;  // received units
     uint8_t* grecv = nullptr; u64 grecv_cap = 0;   // root: the gathered runs
     u64* h_rb = nullptr; u64 h_rb_cap = 0;    // pinned run bounds
@@ -261,8 +266,10 @@ int compact(wcg_ctx* c, bool defer = false) {
     if (defer && !c->two_pass_used && !c->imported && c->nrec_hint >= 2 && !exact_env) {
         const u64 total = c->gslots + c->lslots;
         RC(ensure_recs(c, total));
-        // nrec and nlong are zero here: wcg_reset cleared them, and every one-pass map call's
-        // k_agg zeroes them (a tiny memset dispatch costs ~4 us)
+        // nrec and nlong are zero after wcg_reset and after every one-pass map call's k_agg (a tiny
+        // memset dispatch costs ~4 us); otherwise (a reduce again with no map in between) clear them
+        if (!c->counts_clean) HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));
+        c->counts_clean = false;
         if (c->timing_all) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
         k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
             c->gtab, c->gslots, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st,
@@ -287,6 +294,7 @@ int compact(wcg_ctx* c, bool defer = false) {
         if (scan_gtab && c->glist && c->h_st->gnew <= GLIST_CAP) { glist = c->glist; gs = c->h_st->gnew; }
     }
     if (!scan_gtab) gs = 0;
+    c->counts_clean = false;
     const u64 total = gs + c->lslots;
     const u64 emit_cap = c->max_keys + 65536;     // the log's length: min(nemit, emit_cap)
     if (c->two_pass_used && c->remit) {
@@ -758,10 +766,10 @@ int wcg_close(wcg_ctx* c) {
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
                     c->llog, c->llog_len, c->smp, c->bid, c->spx, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->ovf, c->hist, c->spart, c->ikey, c->iidx, c->groups,
                     c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig,
-                    c->d_xcnt, c->xrecv, c->grecv, c->glist};
+                    c->d_xrow, c->xrecv, c->grecv, c->glist};
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (void* b : bufs) if (b) (void)hipFree(b);
-    if (c->h_xcnt) (void)hipHostFree(c->h_xcnt);
+    if (c->h_x) (void)hipHostFree(c->h_x);
     if (c->h_st) (void)hipHostFree(c->h_st);
     if (c->h_cur) (void)hipHostFree(c->h_cur);
     if (c->h_rb) (void)hipHostFree(c->h_rb);
@@ -870,6 +878,7 @@ int reset_tables(wcg_ctx* c) {
         reinterpret_cast<uint4*>(c->gtab), g16, reinterpret_cast<uint4*>(c->ltab), l16, c->st, glist);
     HIPCHK(c, hipGetLastError());
     c->gtab_zero = true;
+    c->counts_clean = true;
     c->compacted = c->reduced = c->merged = false;
     c->exp_ready = false;
     c->part_R = 0;
@@ -1116,6 +1125,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     if (!two_pass) {
         k_agg<AGG_SPILL><<<nb1, AGG_NT, 0, c->stream>>>(g);
         HIPCHK(c, hipGetLastError());
+        c->counts_clean = true;                // its block 0 zeroed nrec / nlong
         if (g.clk) RC(agg_clock_report(c, g, nb1, grid));
     } else {
     c->two_pass_used = true;
@@ -1208,11 +1218,20 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
     c->phase_ev[0] = c->phase_ev[1] = nullptr;     // set by compact() only when it runs now
     RC(compact(c, true));
     c->merged = false;
-    if (c->timing_all) { c->phase_ev[2] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream)); }
-    RC(sort_records(c));
-    if (c->timing_all) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }
-    RC(format(c, c->sorted, c->nrec, c->arena, FMT_MERGED, 1, 0, merged_bound(c, c->nrec, false), &c->d_out,
-              &c->out_cap, &c->out_len, c->dev_sized ? &c->st->nrec : nullptr));
+    // sort + format; a device-sized job that fails in them leaves no capacity-sized record count
+    // behind for a later export or reduce to trust
+    rc = [&]() -> int {
+        if (c->timing_all) { c->phase_ev[2] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream)); }
+        RC(sort_records(c));
+        if (c->timing_all) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }
+        RC(format(c, c->sorted, c->nrec, c->arena, FMT_MERGED, 1, 0, merged_bound(c, c->nrec, false), &c->d_out,
+                  &c->out_cap, &c->out_len, c->dev_sized ? &c->st->nrec : nullptr));
+        return WCG_OK;
+    }();
+    if (rc) {
+        if (c->dev_sized) { c->dev_sized = false; c->compacted = false; c->nrec = 0; c->out_len = 0; }
+        return rc;
+    }
     if (c->dev_sized) {                            // the counters came back with the size
         c->dev_sized = false;
         c->nrec = c->nkeys = c->h_st->nrec;
@@ -1532,6 +1551,166 @@ int wcg_map_json(wcg_ctx* c, const uint8_t* host_bytes, uint64_t n, uint32_t nre
         }                                                                                   \
     } while (0)
 
+}  // extern "C"
+
+namespace {
+
+// The plan of one rank's part of the shuffle, from the count matrix every rank holds after the
+// count all-gather: m[s * stride + d] = units rank s sends to rank d.  Send side: this rank's
+// units for d sit at soff[d] of its send buffer (k_export_write's cursors start there); receive
+// side: the units from s land at roff[s], in source-rank order.  Pure host arithmetic, shared by
+// wcg_exchange, wcg_exchange_local and wcg_exchange_plan (the CPU tests).
+template <typename T>
+void plan_exchange(const T* m, u64 stride, u32 W, u32 me, T* soff, T* scnt, T* roff, T* rcnt, T* ts, T* tr) {
+    u64 a = 0, b = 0;
+    for (u32 d = 0; d < W; d++) {
+        const u64 s = m[(u64)me * stride + d];
+        if (soff) soff[d] = a;
+        if (scnt) scnt[d] = s;
+        a += s;
+    }
+    for (u32 s = 0; s < W; s++) {
+        const u64 r = m[(u64)s * stride + me];
+        if (roff) roff[s] = b;
+        if (rcnt) rcnt[s] = r;
+        b += r;
+    }
+    if (ts) *ts = a;
+    if (tr) *tr = b;
+}
+
+// Merge's gather: rank p's run lands at off[p] of root's receive buffer (root's own run too: it
+// is copied there, so the runs are back to back in rank order for wcg_merge_runs).
+template <typename T>
+void plan_gather(const T* sizes, u64 stride, u32 W, T* off, T* total) {
+    u64 a = 0;
+    for (u32 p = 0; p < W; p++) {
+        if (off) off[p] = a;
+        a += sizes[(u64)p * stride];
+    }
+    if (total) *total = a;
+}
+
+// Host and device buffers of the exchange for a world of W: a row per rank ([status, caps...,
+// units per owner]), the gathered matrix, the pinned copies and the export cursors.
+constexpr u64 X_HDR = 3;                  // row header: status, then two capacities
+int x_buffers(wcg_ctx* c, u32 W) {
+    if (c->x_world >= W && c->d_xrow) return WCG_OK;
+    if (c->d_xrow) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(c->d_xrow));
+        HIPCHK(c, hipHostFree(c->h_x));
+        c->d_xrow = nullptr; c->h_x = nullptr; c->x_world = 0;
+    }
+    const u64 S = W + X_HDR;
+    // device: row (S), status word (1), matrix (W x S); pinned: row header + status (4), send
+    // offsets (W), matrix (W x S)
+    HIPCHK(c, hipMalloc(&c->d_xrow, (S + 1 + (u64)W * S) * sizeof(u64)));
+    HIPCHK(c, hipHostMalloc(&c->h_x, (4 + W + (u64)W * S) * sizeof(u64), hipHostMallocDefault));
+    c->x_world = W;
+    return WCG_OK;
+}
+u64* x_dstat(wcg_ctx* c) { return c->d_xrow + c->x_world + X_HDR; }
+u64* x_dmat(wcg_ctx* c) { return c->d_xrow + c->x_world + X_HDR + 1; }
+u64* x_hsoff(wcg_ctx* c) { return c->h_x + 4; }
+u64* x_hmat(wcg_ctx* c) { return c->h_x + 4 + c->x_world; }
+
+// Shuffle, local part before any collective: compaction and this rank's units per owner rank
+// into per_rank[0..W) on the device (the caller cleared it)
+int x_count(wcg_ctx* c, u32 nreduce, u32 W, u64* per_rank) {
+    RC(compact(c));
+    const u64 n = c->nrec;
+    RC(ensure(c, &c->owner, &c->owner_cap, n + 1));
+    if (n) {
+        k_export_count<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(c->crec, n, nreduce, W, c->arena,
+                                                                            c->owner, per_rank);
+        HIPCHK(c, hipGetLastError());
+    }
+    return WCG_OK;
+}
+
+// the send buffer (ts units) and the receive buffer (tr units)
+int x_alloc(wcg_ctx* c, u64 ts, u64 tr) {
+    RC(ensure(c, &c->exp_buf, &c->exp_cap, ts + 1));
+    RC(ensure(c, &c->xrecv, &c->xrecv_cap, tr + 1));
+    return WCG_OK;
+}
+
+// the units into the send buffer, owner d's at soff[d] (soff: pinned, c->h_x)
+int x_write(wcg_ctx* c, u32 W, const u64* soff) {
+    if (!c->nrec) return WCG_OK;
+    HIPCHK(c, hipMemcpyAsync(c->d_per_rank + EX_MAX_RANKS, soff, W * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    k_export_write<<<(unsigned)cdiv(c->nrec, EX_TILE), EX_NT, 0, c->stream>>>(
+        c->crec, c->nrec, W, c->owner, c->d_per_rank + EX_MAX_RANKS, c->arena, c->exp_buf);
+    HIPCHK(c, hipGetLastError());
+    return WCG_OK;
+}
+
+// this rank now keeps exactly its own partitions: tables cleared, the tr received units imported
+int x_import(wcg_ctx* c, u64 tr) {
+    RC(reset_tables(c));
+    if (tr) {
+        k_import<<<grid_for(tr, 256, c->ncu * 8), 256, 0, c->stream>>>(c->xrecv, tr, c->gtab, c->gslots - 1, c->ltab,
+                                                                      c->lslots - 1, c->arena, c->arena_cap, c->st);
+        HIPCHK(c, hipGetLastError());
+        c->imported = true;
+    }
+    return WCG_OK;
+}
+
+// Every rank's status went around with its row (column 0 of the gathered matrix): a rank that
+// failed locally has joined the collective anyway, so all ranks see the failure and return it
+// instead of waiting in a send or receive that will not come.
+int x_statuses(wcg_ctx* c, const u64* m, u64 stride, u32 W, int mine, const char* what) {
+    if (mine) return mine;                    // c->err already says why
+    for (u32 p = 0; p < W; p++) {
+        const u64 s = m[(u64)p * stride];
+        if (s) {
+            char buf[160];
+            snprintf(buf, sizeof buf, "%s: rank %u failed (status %llu); no data was exchanged", what, p,
+                     (unsigned long long)s);
+            c->err = buf;
+            return (int)s;
+        }
+    }
+    return WCG_OK;
+}
+
+// After buffers were grown on some ranks (every rank knows whether any did: the capacities came
+// with the rows): one all-reduce(max) of the allocation status before any data moves.
+int x_agree(wcg_ctx* c, int mine, const char* what) {
+    c->h_x[3] = (u64)mine;
+    HIPCHK(c, hipMemcpyAsync(x_dstat(c), c->h_x + 3, sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(c, ncclAllReduce(x_dstat(c), x_dstat(c), 1, ncclUint64, ncclMax, c->comm, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_x + 3, x_dstat(c), sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (mine) return mine;
+    if (c->h_x[3]) {
+        c->err = std::string(what) + ": a peer rank could not allocate its buffers; no data was exchanged";
+        return (int)c->h_x[3];
+    }
+    return WCG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wcg_exchange_plan(const uint64_t* counts, uint32_t world, uint32_t rank, uint64_t* send_off, uint64_t* send_cnt,
+                      uint64_t* recv_off, uint64_t* recv_cnt, uint64_t* totals) {
+    if (!counts || world == 0 || world > EX_MAX_RANKS || rank >= world) return WCG_EINVAL;
+    uint64_t ts = 0, tr = 0;
+    plan_exchange(counts, world, world, rank, send_off, send_cnt, recv_off, recv_cnt, &ts, &tr);
+    if (totals) { totals[0] = ts; totals[1] = tr; }
+    return WCG_OK;
+}
+
+int wcg_gather_plan(const uint64_t* sizes, uint32_t world, uint32_t root, uint64_t* run_off, uint64_t* total) {
+    if (!sizes || world == 0 || world > EX_MAX_RANKS || root >= world) return WCG_EINVAL;
+    plan_gather(sizes, 1, world, run_off, total);
+    return WCG_OK;
+}
+
 int wcg_comm_id(uint8_t* id_out) {
     if (!id_out) return WCG_EINVAL;
     ncclUniqueId u;
@@ -1550,10 +1729,7 @@ int wcg_comm_init(wcg_ctx* c, const uint8_t* id, int rank, int world) {
     int rc = set_dev(c);
     if (rc) return rc;
     if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
-    if (!c->d_xcnt) {
-        HIPCHK(c, hipMalloc(&c->d_xcnt, 4 * EX_MAX_RANKS * sizeof(u64)));
-        HIPCHK(c, hipHostMalloc(&c->h_xcnt, 4 * EX_MAX_RANKS * sizeof(u64), hipHostMallocDefault));
-    }
+    RC(x_buffers(c, (u32)world));
     ncclUniqueId u;
     memcpy(u.internal, id, WCG_COMM_ID_BYTES);
     NCCLCHK(c, ncclCommInitRank(&c->comm, world, u, rank));
@@ -1564,47 +1740,47 @@ int wcg_comm_init(wcg_ctx* c, const uint8_t* id, int rank, int world) {
 
 // The shuffle of mapreduce.go:214-230 / 242-263 between the GPUs of one job: every rank's
 // aggregate leaves as 32-byte units bucketed by owner rank and the owner imports what it
-// receives.  Stream order: compaction -> k_export_count -> ncclAllToAll(unit counts) -> [the one
-// host read: send and receive counts] -> k_export_write into the send buffer -> grouped
-// ncclSend/ncclRecv -> table clear -> k_import.
+// receives.  Stream order: compaction -> k_export_count (into this rank's row) ->
+// ncclAllGather(rows: status, buffer capacities, units per owner) -> [the one host read: the
+// W x W count matrix] -> plan (plan_exchange) -> k_export_write into the send buffer -> grouped
+// ncclSend/ncclRecv -> table clear -> k_import.  A rank that fails before the all-gather (a full
+// table, a bad argument) joins it with its status, and every rank returns that error.
 int wcg_exchange(wcg_ctx* c, uint32_t nreduce, uint64_t* sent, uint64_t* received) {
     if (!c) return WCG_EINVAL;
     if (!c->comm) { c->err = "wcg_exchange before wcg_comm_init"; return WCG_ESTATE; }
-    if (nreduce == 0) { c->err = "wcg_exchange: nreduce 0"; return WCG_EINVAL; }
-    if (c->merged) { c->err = "wcg_exchange after wcg_merge_runs"; return WCG_ESTATE; }
     int rc = set_dev(c);
     if (rc) return rc;
-    const u32 W = (u32)c->comm_world;
+    const u32 W = (u32)c->comm_world, me = (u32)c->comm_rank;
+    const u64 S = W + X_HDR;
     hipEvent_t e0 = mark(c);
-    RC(compact(c));
-    const u64 n = c->nrec;
-    RC(ensure(c, &c->owner, &c->owner_cap, n + 1));
-    HIPCHK(c, hipMemsetAsync(c->d_per_rank, 0, W * sizeof(u64), c->stream));
-    if (n) {
-        k_export_count<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(c->crec, n, nreduce, W, c->arena,
-                                                                            c->owner, c->d_per_rank);
-        HIPCHK(c, hipGetLastError());
-    }
-    NCCLCHK(c, ncclAllToAll(c->d_per_rank, c->d_xcnt, 1, ncclUint64, c->comm, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_xcnt, c->d_per_rank, W * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_xcnt + EX_MAX_RANKS, c->d_xcnt, W * sizeof(u64), hipMemcpyDeviceToHost,
-                             c->stream));
+    int mine = WCG_OK;
+    if (nreduce == 0) { c->err = "wcg_exchange: nreduce 0"; mine = WCG_EINVAL; }
+    else if (c->merged) { c->err = "wcg_exchange after wcg_merge_runs"; mine = WCG_ESTATE; }
+    HIPCHK(c, hipMemsetAsync(c->d_xrow + X_HDR, 0, W * sizeof(u64), c->stream));
+    if (!mine) mine = x_count(c, nreduce, W, c->d_xrow + X_HDR);
+    u64* hdr = c->h_x;
+    hdr[0] = (u64)mine; hdr[1] = c->exp_buf ? c->exp_cap : 0; hdr[2] = c->xrecv ? c->xrecv_cap : 0;
+    HIPCHK(c, hipMemcpyAsync(c->d_xrow, hdr, X_HDR * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(c, ncclAllGather(c->d_xrow, x_dmat(c), S, ncclUint64, c->comm, c->stream));
+    u64* m = x_hmat(c);
+    HIPCHK(c, hipMemcpyAsync(m, x_dmat(c), (u64)W * S * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));     // the one host read of the exchange
-    const u64* scnt = c->h_xcnt;
-    const u64* rcnt = c->h_xcnt + EX_MAX_RANKS;
-    u64* soff = c->h_xcnt + 2 * EX_MAX_RANKS;       // send offsets (also the export cursors)
-    u64* roff = c->h_xcnt + 3 * EX_MAX_RANKS;
+    RC(x_statuses(c, m, S, W, mine, "wcg_exchange"));
+    std::vector<u64> scnt(W), roff(W), rcnt(W);
+    u64* soff = x_hsoff(c);
     u64 ts = 0, tr = 0;
-    for (u32 p = 0; p < W; p++) { soff[p] = ts; ts += scnt[p]; roff[p] = tr; tr += rcnt[p]; }
-    RC(ensure(c, &c->exp_buf, &c->exp_cap, ts + 1));
-    RC(ensure(c, &c->xrecv, &c->xrecv_cap, tr + 1));
-    if (n) {
-        HIPCHK(c, hipMemcpyAsync(c->d_per_rank + EX_MAX_RANKS, soff, W * sizeof(u64), hipMemcpyHostToDevice,
-                                 c->stream));
-        k_export_write<<<(unsigned)cdiv(n, EX_TILE), EX_NT, 0, c->stream>>>(
-            c->crec, n, W, c->owner, c->d_per_rank + EX_MAX_RANKS, c->arena, c->exp_buf);
-        HIPCHK(c, hipGetLastError());
+    plan_exchange<u64>(m + X_HDR, S, W, me, soff, scnt.data(), roff.data(), rcnt.data(), &ts, &tr);
+    // does any rank grow a buffer?  (all ranks decide alike: the capacities came with the rows)
+    bool grow = false;
+    for (u32 p = 0; p < W && !grow; p++) {
+        u64 tsp = 0, trp = 0;
+        plan_exchange<u64>(m + X_HDR, S, W, p, nullptr, nullptr, nullptr, nullptr, &tsp, &trp);
+        grow = tsp + 1 > m[(u64)p * S + 1] || trp + 1 > m[(u64)p * S + 2];
     }
+    const int arc = x_alloc(c, ts, tr);
+    if (grow) RC(x_agree(c, arc, "wcg_exchange"));
+    else RC(arc);
+    RC(x_write(c, W, soff));
     hipEvent_t e1 = mark(c);
     NCCLCHK(c, ncclGroupStart());
     for (u32 p = 0; p < W; p++) {
@@ -1615,14 +1791,7 @@ int wcg_exchange(wcg_ctx* c, uint32_t nreduce, uint64_t* sent, uint64_t* receive
     }
     NCCLCHK(c, ncclGroupEnd());
     hipEvent_t e2 = mark(c);
-    // this rank now holds exactly its own partitions
-    RC(reset_tables(c));
-    if (tr) {
-        k_import<<<grid_for(tr, 256, c->ncu * 8), 256, 0, c->stream>>>(c->xrecv, tr, c->gtab, c->gslots - 1, c->ltab,
-                                                                      c->lslots - 1, c->arena, c->arena_cap, c->st);
-        HIPCHK(c, hipGetLastError());
-        c->imported = true;
-    }
+    RC(x_import(c, tr));
     hipEvent_t e3 = mark(c);
     record_x(c, 5, e0, e1);
     record_x(c, 6, e1, e2);
@@ -1633,27 +1802,37 @@ int wcg_exchange(wcg_ctx* c, uint32_t nreduce, uint64_t* sent, uint64_t* receive
 }
 
 // Merge (mapreduce.go:284-321) across the ranks: the owners' sorted runs (disjoint key sets)
-// travel to root, which merges them without a re-sort (wcg_merge_runs).
+// travel to root, which merges them without a re-sort (wcg_merge_runs).  Rows of the all-gather:
+// {status, run bytes, root's receive capacity}.
 int wcg_gather_merge(wcg_ctx* c, int root, uint64_t* nkeys, uint64_t* nbytes) {
     if (!c) return WCG_EINVAL;
     if (!c->comm) { c->err = "wcg_gather_merge before wcg_comm_init"; return WCG_ESTATE; }
     if (root < 0 || root >= c->comm_world) { c->err = "wcg_gather_merge: bad root"; return WCG_EINVAL; }
-    if (!c->reduced || c->merged) { c->err = "wcg_gather_merge needs a wcg_reduce result"; return WCG_ESTATE; }
     int rc = set_dev(c);
     if (rc) return rc;
     const u32 W = (u32)c->comm_world;
     const bool am_root = c->comm_rank == root;
+    const u64 S = 3;
     hipEvent_t e0 = mark(c);
-    u64* d_mine = c->d_xcnt + 2 * EX_MAX_RANKS;
-    u64* d_all = c->d_xcnt + 3 * EX_MAX_RANKS;
-    c->h_xcnt[2 * EX_MAX_RANKS] = c->out_len;
-    HIPCHK(c, hipMemcpyAsync(d_mine, c->h_xcnt + 2 * EX_MAX_RANKS, sizeof(u64), hipMemcpyHostToDevice, c->stream));
-    NCCLCHK(c, ncclAllGather(d_mine, d_all, 1, ncclUint64, c->comm, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_xcnt, d_all, W * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    int mine = WCG_OK;
+    if (!c->reduced || c->merged) { c->err = "wcg_gather_merge needs a wcg_reduce result"; mine = WCG_ESTATE; }
+    u64* hdr = c->h_x;
+    hdr[0] = (u64)mine; hdr[1] = mine ? 0 : c->out_len; hdr[2] = c->grecv ? c->grecv_cap : 0;
+    HIPCHK(c, hipMemcpyAsync(c->d_xrow, hdr, S * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(c, ncclAllGather(c->d_xrow, x_dmat(c), S, ncclUint64, c->comm, c->stream));
+    u64* m = x_hmat(c);
+    HIPCHK(c, hipMemcpyAsync(m, x_dmat(c), (u64)W * S * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));     // the run sizes (one host read)
-    std::vector<uint64_t> sizes(c->h_xcnt, c->h_xcnt + W);
+    RC(x_statuses(c, m, S, W, mine, "wcg_gather_merge"));
+    std::vector<uint64_t> sizes(W);
+    std::vector<u64> off(W);
+    for (u32 p = 0; p < W; p++) sizes[p] = m[(u64)p * S + 1];
     u64 total = 0;
-    for (uint64_t s : sizes) total += s;
+    plan_gather<u64>(m + 1, S, W, off.data(), &total);
+    const bool grow = total + 64 > m[(u64)root * S + 2];
+    const int arc = am_root ? ensure(c, &c->grecv, &c->grecv_cap, total + 64) : WCG_OK;
+    if (grow) RC(x_agree(c, arc, "wcg_gather_merge"));
+    else RC(arc);
     if (!am_root) {
         if (c->out_len)
             NCCLCHK(c, ncclSend(c->d_out, c->out_len, ncclUint8, root, c->comm, c->stream));
@@ -1663,24 +1842,93 @@ int wcg_gather_merge(wcg_ctx* c, int root, uint64_t* nkeys, uint64_t* nbytes) {
         if (nbytes) *nbytes = 0;
         return WCG_OK;
     }
-    RC(ensure(c, &c->grecv, &c->grecv_cap, total + 64));
-    u64 off = 0;
     NCCLCHK(c, ncclGroupStart());
-    for (u32 p = 0; p < W; p++) {
+    for (u32 p = 0; p < W; p++)
         if (sizes[p] && (int)p != root)
-            NCCLCHK(c, ncclRecv(c->grecv + off, sizes[p], ncclUint8, (int)p, c->comm, c->stream));
-        off += sizes[p];
-    }
+            NCCLCHK(c, ncclRecv(c->grecv + off[p], sizes[p], ncclUint8, (int)p, c->comm, c->stream));
     NCCLCHK(c, ncclGroupEnd());
-    off = 0;
-    for (u32 p = 0; p < (u32)root; p++) off += sizes[p];
-    if (sizes[root]) HIPCHK(c, hipMemcpyAsync(c->grecv + off, c->d_out, sizes[root], hipMemcpyDeviceToDevice, c->stream));
+    if (sizes[root])
+        HIPCHK(c, hipMemcpyAsync(c->grecv + off[root], c->d_out, sizes[root], hipMemcpyDeviceToDevice, c->stream));
     hipEvent_t e1 = mark(c);
     RC(wcg_merge_runs(c, c->grecv, sizes.data(), W, nkeys, nbytes));
     hipEvent_t e2 = mark(c);
     record_x(c, 8, e0, e1);
     record_x(c, 9, e1, e2);
     return WCG_OK;
+}
+
+// ---- the same shuffle and Merge across the contexts of one process (a test transport): every
+// step but the transport is the code above - the count matrix, plan_exchange / plan_gather, the
+// export, import and merge kernels; device copies stand in for ncclSend / ncclRecv.
+int wcg_exchange_local(wcg_ctx** cs, uint32_t W, uint32_t nreduce, uint64_t* sent, uint64_t* received) {
+    if (!cs || W == 0 || W > EX_MAX_RANKS || nreduce == 0) return WCG_EINVAL;
+    for (u32 p = 0; p < W; p++) {
+        if (!cs[p]) return WCG_EINVAL;
+        for (u32 q = 0; q < p; q++) if (cs[q] == cs[p]) return WCG_EINVAL;
+        if (cs[p]->merged) { cs[p]->err = "wcg_exchange_local after wcg_merge_runs"; return WCG_ESTATE; }
+    }
+    std::vector<u64> m((u64)W * W);
+    for (u32 p = 0; p < W; p++) {
+        wcg_ctx* c = cs[p];
+        RC(set_dev(c));
+        RC(x_buffers(c, W));
+        HIPCHK(c, hipMemsetAsync(c->d_xrow + X_HDR, 0, W * sizeof(u64), c->stream));
+        RC(x_count(c, nreduce, W, c->d_xrow + X_HDR));
+        HIPCHK(c, hipMemcpyAsync(x_hmat(c), c->d_xrow + X_HDR, W * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        std::copy(x_hmat(c), x_hmat(c) + W, m.begin() + (u64)p * W);
+    }
+    std::vector<u64> roff((u64)W * W), ts(W), tr(W);
+    for (u32 p = 0; p < W; p++) {
+        wcg_ctx* c = cs[p];
+        RC(set_dev(c));
+        plan_exchange<u64>(m.data(), W, W, p, x_hsoff(c), nullptr, roff.data() + (u64)p * W, nullptr, &ts[p], &tr[p]);
+        RC(x_alloc(c, ts[p], tr[p]));
+        RC(x_write(c, W, x_hsoff(c)));
+    }
+    for (u32 p = 0; p < W; p++) { RC(set_dev(cs[p])); HIPCHK(cs[p], hipStreamSynchronize(cs[p]->stream)); }
+    for (u32 d = 0; d < W; d++) {
+        wcg_ctx* c = cs[d];
+        RC(set_dev(c));
+        for (u32 s = 0; s < W; s++) {
+            const u64 n = m[(u64)s * W + d];
+            if (n)
+                HIPCHK(c, hipMemcpyAsync(c->xrecv + roff[(u64)d * W + s], cs[s]->exp_buf + x_hsoff(cs[s])[d],
+                                         n * sizeof(Rec), hipMemcpyDeviceToDevice, c->stream));
+        }
+        RC(x_import(c, tr[d]));
+    }
+    for (u32 p = 0; p < W; p++) {
+        RC(set_dev(cs[p]));
+        HIPCHK(cs[p], hipStreamSynchronize(cs[p]->stream));   // the send buffers are free again
+        if (sent) sent[p] = ts[p];
+        if (received) received[p] = tr[p];
+    }
+    return WCG_OK;
+}
+
+int wcg_gather_merge_local(wcg_ctx** cs, uint32_t W, uint32_t root, uint64_t* nkeys, uint64_t* nbytes) {
+    if (!cs || W == 0 || W > EX_MAX_RANKS || root >= W) return WCG_EINVAL;
+    std::vector<uint64_t> sizes(W), off(W);
+    for (u32 p = 0; p < W; p++) {
+        if (!cs[p]) return WCG_EINVAL;
+        if (!cs[p]->reduced || cs[p]->merged) { cs[p]->err = "wcg_gather_merge_local needs a wcg_reduce result"; return WCG_ESTATE; }
+        sizes[p] = cs[p]->out_len;
+    }
+    uint64_t total = 0;
+    plan_gather(sizes.data(), 1, W, off.data(), &total);
+    wcg_ctx* r = cs[root];
+    RC(set_dev(r));
+    RC(ensure(r, &r->grecv, &r->grecv_cap, total + 64));
+    for (u32 p = 0; p < W; p++) {
+        RC(set_dev(cs[p]));
+        HIPCHK(cs[p], hipStreamSynchronize(cs[p]->stream));
+    }
+    RC(set_dev(r));
+    for (u32 p = 0; p < W; p++)
+        if (sizes[p])
+            HIPCHK(r, hipMemcpyAsync(r->grecv + off[p], cs[p]->d_out, sizes[p], hipMemcpyDeviceToDevice, r->stream));
+    return wcg_merge_runs(r, r->grecv, sizes.data(), W, nkeys, nbytes);
 }
 
 int wcg_timings(wcg_ctx* c, double* ms, int n, uint64_t* map_launches) {

@@ -3,4 +3,5 @@
 Python host side (tests, bench, multi-GPU orchestration) over the C ABI of libwcg.so
 (include/wcg.h).  The compute path is hand-written HIP for gfx950; there is no CPU fallback.
 """
-from ._lib import Engine, WcgError, ihash, load, version, EXPORTED, RECORD_BYTES  # noqa: F401
+from ._lib import (Engine, WcgError, ihash, load, version, EXPORTED, RECORD_BYTES,  # noqa: F401
+                   exchange_plan, gather_plan, exchange_local, gather_merge_local)

@@ -25,7 +25,8 @@ EXPORTED = [
     "wcg_export", "wcg_import", "wcg_timings", "wcg_enable_timing", "wcg_stats", "wcg_ihash",
     "wcg_version", "wcg_map_file", "wcg_partition_all", "wcg_map_json", "wcg_export_count",
     "wcg_export_write", "wcg_merge_runs", "wcg_result_copy_device", "wcg_sync", "wcg_free",
-    "wcg_comm_id", "wcg_comm_init", "wcg_exchange", "wcg_gather_merge",
+    "wcg_comm_id", "wcg_comm_init", "wcg_exchange", "wcg_gather_merge", "wcg_exchange_plan",
+    "wcg_gather_plan", "wcg_exchange_local", "wcg_gather_merge_local",
 ]
 COMM_ID_BYTES = 128
 
@@ -79,6 +80,10 @@ def load() -> ctypes.CDLL:
         "wcg_comm_init": (I, [P, P, I, I]),
         "wcg_exchange": (I, [P, U32, PU64, PU64]),
         "wcg_gather_merge": (I, [P, I, PU64, PU64]),
+        "wcg_exchange_plan": (I, [PU64, U32, U32, PU64, PU64, PU64, PU64, PU64]),
+        "wcg_gather_plan": (I, [PU64, U32, U32, PU64, PU64]),
+        "wcg_exchange_local": (I, [ctypes.POINTER(P), U32, U32, PU64, PU64]),
+        "wcg_gather_merge_local": (I, [ctypes.POINTER(P), U32, U32, PU64, PU64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -353,6 +358,58 @@ def _slices(raw: bytes, sizes: List[int]) -> List[bytes]:
         out.append(raw[off:off + n])
         off += n
     return out
+
+
+def exchange_plan(counts: List[List[int]], rank: int) -> dict:
+    """wcg_exchange_plan: counts[s][d] = units rank s sends to rank d -> this rank's send / receive
+    offsets and counts (host arithmetic, no GPU)."""
+    W = len(counts)
+    flat = (ctypes.c_uint64 * (W * W))(*[int(x) for row in counts for x in row])
+    so, sc, ro, rc = [(ctypes.c_uint64 * W)() for _ in range(4)]
+    tot = (ctypes.c_uint64 * 2)()
+    st = load().wcg_exchange_plan(flat, W, rank, so, sc, ro, rc, tot)
+    if st != WCG_OK:
+        raise WcgError(st, "wcg_exchange_plan: bad arguments")
+    return {"send_off": list(so), "send_cnt": list(sc), "recv_off": list(ro), "recv_cnt": list(rc),
+            "sent": tot[0], "received": tot[1]}
+
+
+def gather_plan(sizes: List[int], root: int) -> Tuple[List[int], int]:
+    """wcg_gather_plan: where each rank's run lands in root's receive buffer, and the total."""
+    W = len(sizes)
+    sz = (ctypes.c_uint64 * max(W, 1))(*sizes)
+    off = (ctypes.c_uint64 * max(W, 1))()
+    tot = ctypes.c_uint64()
+    st = load().wcg_gather_plan(sz, W, root, off, ctypes.byref(tot))
+    if st != WCG_OK:
+        raise WcgError(st, "wcg_gather_plan: bad arguments")
+    return list(off)[:W], tot.value
+
+
+def _ctx_array(engines: List["Engine"]):
+    return (ctypes.c_void_p * len(engines))(*[e._ctx.value for e in engines])
+
+
+def exchange_local(engines: List["Engine"], nreduce: int) -> Tuple[List[int], List[int]]:
+    """wcg_exchange_local: the shuffle across engines of this process (a world of len(engines)
+    ranks, device copies for transport).  Returns (units sent, units received) per engine."""
+    W = len(engines)
+    snt, rcv = (ctypes.c_uint64 * W)(), (ctypes.c_uint64 * W)()
+    st = load().wcg_exchange_local(_ctx_array(engines), W, nreduce, snt, rcv)
+    if st != WCG_OK:
+        msgs = "; ".join(load().wcg_last_error(e._ctx).decode() for e in engines)
+        raise WcgError(st, f"wcg_exchange_local: {msgs}")
+    return list(snt), list(rcv)
+
+
+def gather_merge_local(engines: List["Engine"], root: int) -> Tuple[int, int]:
+    """wcg_gather_merge_local: every engine's sorted run merged into engines[root]'s result."""
+    nk, nb = ctypes.c_uint64(), ctypes.c_uint64()
+    st = load().wcg_gather_merge_local(_ctx_array(engines), len(engines), root, ctypes.byref(nk), ctypes.byref(nb))
+    if st != WCG_OK:
+        msgs = "; ".join(load().wcg_last_error(e._ctx).decode() for e in engines)
+        raise WcgError(st, f"wcg_gather_merge_local: {msgs}")
+    return nk.value, nb.value
 
 
 def version() -> str:

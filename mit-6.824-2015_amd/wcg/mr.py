@@ -306,7 +306,12 @@ class Worker:
     def Shutdown(self, a: dict) -> dict:                    # worker.go:36-44
         self.nrpc = 0                       # stop accepting (closing the listener ends accept())
         self.l.close()
-        return {"Njobs": self.njobs - 1, "OK": True}        # don't count the Shutdown RPC
+        # worker.go:40-43: the reply carries nJobs as it stands - the Shutdown RPC's own
+        # connection included - and only then is that connection uncounted (wk.nJobs--), so
+        # KillWorkers' list holds jobs + 1 per worker, as the reference's does
+        njobs = self.njobs
+        self.njobs -= 1
+        return {"Njobs": njobs, "OK": True}
 
     def _serve(self) -> None:
         handlers = {"Worker.DoJob": self.DoJob, "Worker.Shutdown": self.Shutdown}

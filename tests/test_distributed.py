@@ -165,3 +165,47 @@ def test_line_aligned_ranges():
     assert rs[0][0] == 0 and rs[-1][1] == len(data)
     for (a, b), (c, d) in zip(rs, rs[1:]):
         assert b == c and (b == 0 or data[b - 1] == 0x0A)
+
+
+# ---------------------------------------------------------------- the rank launcher of bench.py
+def _launch(nprocs, extra, timeout=120):
+    import io
+    from wcg.launch import launch_ranks
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "standin_rank.py")
+    buf = io.StringIO()
+    rc = launch_ranks(script, extra, nprocs, timeout, out=buf)
+    return rc, buf.getvalue()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_launcher_runs_every_rank(world):
+    """`bench.py --gpus N` without an external launcher: the parent starts N ranks (before any GPU
+    call), relays rank 0's one JSON line and exits 0."""
+    import json
+    rc, out = _launch(world, [])
+    assert rc == 0, out
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == world and rec["verified_vs_oracle"] is True
+
+
+def test_launcher_reports_a_failed_rank():
+    rc, out = _launch(2, ["--fail-rank", "1"])
+    assert rc != 0
+    assert not [l for l in out.splitlines() if l.startswith("{")]
+
+
+def test_launcher_bounds_a_hung_rank():
+    import time
+    t0 = time.time()
+    rc, out = _launch(2, ["--hang-rank", "1"], timeout=20)
+    assert rc != 0
+    assert time.time() - t0 < 60
+
+
+def test_bench_self_launches_before_any_gpu_call():
+    """bench.py hands `--gpus N` without WORLD_SIZE to the launcher before importing torch."""
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")).read()
+    main = src[src.index("def main():"):]
+    assert main.index("launch_ranks(") < main.index("import torch")

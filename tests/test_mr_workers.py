@@ -131,6 +131,8 @@ def test_master_workers_cpu_standin(tmp_path, name, schedule):
     job, workers = _run(tmp_path, StandInEngine, nmap=20, nreduce=10, schedule=schedule)
     if name == "basic":                     # checkWorker: every worker did at least one job
         assert len(job.stats) == 2 and all(n > 0 for n in job.stats), job.stats
+        # worker.go:40-43: each worker's Njobs counts its DoJob connections plus the Shutdown RPC's
+        assert sum(job.stats) == 20 + 10 + 2, job.stats
 
 
 def test_split_matches_reference_rules(tmp_path):
