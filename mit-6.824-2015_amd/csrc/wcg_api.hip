@@ -43,6 +43,7 @@ struct wcg_ctx {
     GEntry* gtab = nullptr; u64 gslots = 0;
     GEntry* ltab = nullptr; u64 lslots = 0;
     uint8_t* arena = nullptr; u64 arena_cap = 0;
+    u64 lheap_cap = 0;                        // two-pass contexts: the log heap after arena_cap
     DevState* st = nullptr;
     DevState* h_st = nullptr;                 // pinned mirror
     Rec* recA = nullptr; Rec* recB = nullptr; u64 rec_cap = 0;
@@ -80,6 +81,8 @@ struct wcg_ctx {
     bool two_pass_used = false;               // a map call since wcg_reset ran the two passes
     bool gtab_zero = false;                   // the global table was cleared by the last wcg_reset
     u64* glist = nullptr;                     // two-pass contexts: claimed global-table slots
+    u64* llist = nullptr;                     // large contexts: claimed long-key-table slots
+    bool ltab_zero = false;                   // the long-key table was cleared and nothing claimed since
     bool imported = false;                    // wcg_import since wcg_reset
     u32* lpcur = nullptr; u64 lpcur_cap = 0;    // 2n records: by bucket, and the oversized-bucket scratch
     u32* hist = nullptr; u64 hist_cap = 0;    // [B][G] bucket counts / partition counts
@@ -287,22 +290,29 @@ int compact(wcg_ctx* c, bool defer = false) {
     bool scan_gtab = true;
     const u64* glist = nullptr;                    // the listed claims instead of the whole table
     u64 gs = c->gslots;
-    if (c->two_pass_used && !c->imported) {
+    const u64* llist = nullptr;
+    u64 ls = c->lslots;
+    if ((c->two_pass_used && !c->imported) || c->llist) {
         HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        scan_gtab = c->h_st->global_ops != 0;
-        if (scan_gtab && c->glist && c->h_st->gnew <= GLIST_CAP) { glist = c->glist; gs = c->h_st->gnew; }
+        if (c->two_pass_used && !c->imported) {
+            scan_gtab = c->h_st->global_ops != 0;
+            if (scan_gtab && c->glist && c->h_st->gnew <= GLIST_CAP) { glist = c->glist; gs = c->h_st->gnew; }
+        }
+        // listed long-key claims (the table was cleared by a listed or full clear since: every
+        // claim since is listed while lnew <= LLIST_CAP)
+        if (c->llist && c->ltab_zero && c->h_st->lnew <= LLIST_CAP) { llist = c->llist; ls = c->h_st->lnew; }
     }
     if (!scan_gtab) gs = 0;
     c->counts_clean = false;
-    const u64 total = gs + c->lslots;
+    const u64 total = gs + ls;
     const u64 emit_cap = c->max_keys + 65536;     // the log's length: min(nemit, emit_cap)
     if (c->two_pass_used && c->remit) {
         HIPCHK(c, hipMemsetAsync(&c->st->nlong, 0, sizeof(u64), c->stream));
         if (c->timing_all) { c->phase_ev[0] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[0], c->stream)); }
         k_log_len<<<1, 1, 0, c->stream>>>(emit_cap, c->st);
-        k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
-            c->gtab, gs, c->ltab, c->lslots, c->arena, c->remit, c->remit_cap, c->st, nullptr, glist);
+        k_compact<<<(unsigned)cdiv(std::max<u64>(total, 1), CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
+            c->gtab, gs, c->ltab, ls, c->arena, c->remit, c->remit_cap, c->st, nullptr, glist, llist);
         HIPCHK(c, hipGetLastError());
         if (c->timing_all) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
         RC(check_status(c));
@@ -321,8 +331,8 @@ int compact(wcg_ctx* c, bool defer = false) {
                                             // two-pass map calls write it)
             k_copy_emit<<<(unsigned)(c->ncu * 4), 256, 0, c->stream>>>(
                 c->remit, c->recA, std::min<u64>(c->rec_cap, emit_cap), c->st);
-        k_compact<<<(unsigned)cdiv(total, CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
-            c->gtab, gs, c->ltab, c->lslots, c->arena, c->recA, c->rec_cap, c->st, nullptr, glist);
+        k_compact<<<(unsigned)cdiv(std::max<u64>(total, 1), CP_NT * CP_IPT), CP_NT, 0, c->stream>>>(
+            c->gtab, gs, c->ltab, ls, c->arena, c->recA, c->rec_cap, c->st, nullptr, glist, llist);
         HIPCHK(c, hipGetLastError());
         if (c->timing_all) { c->phase_ev[1] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[1], c->stream)); }
         RC(check_status(c));
@@ -390,7 +400,7 @@ int ensure_items(wcg_ctx* c, u64 n2) {
 
 // long keys sharing a 16-byte prefix in r[0:n): ordered by their full bytes (key bytes at
 // `base`); `tmp` is a free record buffer of n records
-int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64* nd = nullptr) {
+int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64* nd = nullptr, u64* nkeys = nullptr) {
     if (n < 2) return WCG_OK;
     RC(ensure(c, &c->groups, &c->groups_cap, n / 2 + 2));
     RC(ensure_items(c, 2 * n));
@@ -399,7 +409,7 @@ int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64
     k_tie_mark<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(r, n, nd, c->groups, ng);
     TieArgs t;
     t.r = r; t.n = n; t.nd = nd; t.base = base; t.groups = c->groups; t.ngroups = ng;
-    t.tmp = tmp; t.sc_key = c->ikey; t.sc_pos = c->iidx;
+    t.tmp = tmp; t.sc_key = c->ikey; t.sc_pos = c->iidx; t.nkeys = nkeys;
     k_tie_sort<<<(unsigned)c->ncu, TG_NT, 0, c->stream>>>(t);
     HIPCHK(c, hipGetLastError());
     return WCG_OK;
@@ -481,7 +491,11 @@ int sort_records(wcg_ctx* c) {
         k_ss_split<<<cdiv(a.B, 256), 256, 0, c->stream>>>(a);
     }
     if (small) k_ss_hist<true><<<a.G, SS_NT, 0, c->stream>>>(a);
-    else k_ss_hist<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
+    else if (WCG_SS_SPLIT && tr) {                 // r04: the search, then the histogram (wcg_sort.h)
+        k_ss_find<<<(unsigned)std::max<u64>(1, std::min<u64>(cdiv(np, SSF_NT * SS_U), (u64)c->ncu * 2)), SSF_NT, 0,
+                    c->stream>>>(a);
+        k_ss_count<<<a.G, SSL_NT, 0, c->stream>>>(a);
+    } else k_ss_hist<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
     if (tr) {
         k_ss_colscan<<<cdiv(a.B, 256), 256, 0, c->stream>>>(a.hist, a.B, a.G, a.bstart);
@@ -494,11 +508,14 @@ int sort_records(wcg_ctx* c) {
     k_ss_bucket<false><<<a.B, SB_NT, 0, c->stream>>>(a);
     k_ss_bucket<true><<<a.B, SB_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
-    if (dev || c->h_st->nlong >= 2) RC(fix_ties(c, c->recB, n, c->arena, c->recA, a.nd));
+    // long records: from the table (nlong) and, in two-pass jobs, from the record log (lemit)
+    if (dev || c->h_st->nlong + c->h_st->lemit >= 2)
+        RC(fix_ties(c, c->recB, n, c->arena, c->recA, a.nd, a.dedupe ? a.nkeys : nullptr));
     if (c->crec == c->recA) c->compacted = false;    // recA was scratch for the ties
     if (getenv("WCG_DEBUG"))
-        fprintf(stderr, "wcg: nemit %llu global_ops %llu\n", (unsigned long long)c->h_st->nemit,
-                (unsigned long long)c->h_st->global_ops);
+        fprintf(stderr, "wcg: nemit %llu global_ops %llu long fallbacks %u long claims %llu\n",
+                (unsigned long long)c->h_st->nemit, (unsigned long long)c->h_st->global_ops, c->h_st->long_fb,
+                (unsigned long long)c->h_st->lnew);
     c->nkeys = n;
     // record-log jobs count their distinct keys on the device (d_scalar[8]); the count is read
     // with the formatted size at the end of wcg_reduce (one host round trip fewer)
@@ -539,7 +556,8 @@ int format(wcg_ctx* c, const Rec* r, u64 n, const uint8_t* base, int fmt, u32 nr
 u64 merged_bound(wcg_ctx* c, u64 n, bool json) {
     // inline keys <= 15 bytes; long keys <= 32 bytes in their cell, longer ones on the heap (its
     // used part is not known on the host in a device-sized job: the whole heap)
-    return n * (LONG_CELL + (json ? JSON_FIXED : 3) + 20) + (c->dev_sized ? c->arena_cap : c->h_st->arena_top) + 64;
+    return n * (LONG_CELL + (json ? JSON_FIXED : 3) + 20) +
+           (c->dev_sized ? c->arena_cap : c->h_st->arena_top + c->h_st->lheap_top) + 64;
 }
 
 // every -res-<r> for nreduce R, back to back in c->d_part (cached until the next job)
@@ -716,9 +734,12 @@ int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx** 
     c->gslots = next_pow2(2 * c->max_keys);
     c->lslots = std::max<u64>(next_pow2(c->gslots / 4), 4096);
     c->arena_cap = std::max<u64>(64ull << 20, c->lslots * 32);   // heap part (after the slot cells)
+    // two-pass (high-cardinality) contexts: k_long_agg puts long keys straight into the record log,
+    // their bytes on a heap of their own (at least one 32-byte cell each): room for a full log
+    if (c->max_keys > (4ull << 20)) c->lheap_cap = 32 * (c->max_keys + 65536);
     HIPCHK(c, hipMalloc(&c->gtab, c->gslots * sizeof(GEntry)));
     HIPCHK(c, hipMalloc(&c->ltab, c->lslots * sizeof(GEntry)));
-    HIPCHK(c, hipMalloc(&c->arena, c->lslots * LONG_CELL + c->arena_cap + 64));
+    HIPCHK(c, hipMalloc(&c->arena, c->lslots * LONG_CELL + c->arena_cap + c->lheap_cap + 64));
     // DevState and the scalars (scan totals, the tie-group count) in one block, so that one copy
     // reads a device-sized job's counters and sizes back
     static_assert(sizeof(DevState) <= ST_SCALAR_OFF, "DevState fits before the scalars");
@@ -736,6 +757,10 @@ int wcg_open(int device, uint64_t max_input_bytes, uint64_t max_keys, wcg_ctx** 
     if (c->max_keys > (4ull << 20)) {
         HIPCHK(c, hipMalloc(&c->glist, GLIST_CAP * sizeof(u64)));
         HIPCHK(c, hipMemcpy(c->d_scalar + ST_GLIST, &c->glist, sizeof(u64*), hipMemcpyHostToDevice));
+        // ... and their long-key table's claims (C4: 1.6M of 16M slots per GiB; clearing and
+        // compacting the whole 512 MiB table took 0.13 + ~0.15 ms of a 9.6 ms job)
+        HIPCHK(c, hipMalloc(&c->llist, LLIST_CAP * sizeof(u64)));
+        HIPCHK(c, hipMemcpy(c->d_scalar + ST_LLIST, &c->llist, sizeof(u64*), hipMemcpyHostToDevice));
     }
     // records: compaction output is bounded by the number of occupied slots
     c->rec_cap = c->max_keys + 65536;
@@ -766,7 +791,7 @@ int wcg_close(wcg_ctx* c) {
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
                     c->llog, c->llog_len, c->smp, c->bid, c->spx, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->ovf, c->hist, c->spart, c->ikey, c->iidx, c->groups,
                     c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig,
-                    c->d_xrow, c->xrecv, c->grecv, c->glist};
+                    c->d_xrow, c->xrecv, c->grecv, c->glist, c->llist};
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_x) (void)hipHostFree(c->h_x);
@@ -860,24 +885,42 @@ int reset_tables(wcg_ctx* c) {
     bool clear_g = true;
     const u64* glist = nullptr;                    // clear only the listed claims
     u64 g16 = c->gslots * sizeof(GEntry) / 16;
+    bool have_st = false;
+    auto read_st = [&]() -> int {
+        if (have_st) return WCG_OK;
+        HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        have_st = true;
+        return WCG_OK;
+    };
+    const bool touched = c->map_launches_since_reset != 0 || c->imported;
     if (c->gtab_zero && !c->imported) {
         if (c->map_launches_since_reset == 0) clear_g = false;
         else if (c->two_pass_used) {
-            HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
+            RC(read_st());
             clear_g = c->h_st->global_ops != 0;
             if (clear_g && c->glist && c->h_st->gnew <= GLIST_CAP) { glist = c->glist; g16 = 2 * c->h_st->gnew; }
+        }
+    }
+    // the long-key table: untouched since its last clear, or (large contexts) its listed claims
+    const u64* llist = nullptr;
+    u64 l16 = c->lslots * sizeof(GEntry) / 16;
+    if (c->llist && c->ltab_zero) {
+        if (!touched) l16 = 0;
+        else {
+            RC(read_st());
+            if (c->h_st->lnew <= LLIST_CAP) { llist = c->llist; l16 = 2 * c->h_st->lnew; }
         }
     }
     c->map_launches_since_reset = 0;
     // one launch clears the tables and the counters (three memsets were three dispatches)
     if (!clear_g) g16 = 0;
-    const u64 l16 = c->lslots * sizeof(GEntry) / 16;
     static_assert(sizeof(GEntry) == 32, "k_clear's listed entries are two 16-byte words");
     k_clear<<<grid_for(g16 + l16, 256, c->ncu * 4), 256, 0, c->stream>>>(
-        reinterpret_cast<uint4*>(c->gtab), g16, reinterpret_cast<uint4*>(c->ltab), l16, c->st, glist);
+        reinterpret_cast<uint4*>(c->gtab), g16, reinterpret_cast<uint4*>(c->ltab), l16, c->st, glist, llist);
     HIPCHK(c, hipGetLastError());
     c->gtab_zero = true;
+    c->ltab_zero = true;
     c->counts_clean = true;
     c->compacted = c->reduced = c->merged = false;
     c->exp_ready = false;
@@ -960,7 +1003,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     a.tiles_per_wg = MAP_WAVES * ((a.ntiles + grid * MAP_WAVES - 1) / (grid * MAP_WAVES));
     a.gtab = c->gtab; a.gmask = c->gslots - 1;
     a.ltab = c->ltab; a.lmask = c->lslots - 1;
-    a.arena = c->arena; a.arena_cap = c->arena_cap;
+    a.arena = c->arena; a.arena_cap = c->arena_cap; a.lheap_cap = c->lheap_cap;
     a.st = c->st;
     // miss log: one region per (workgroup, bucket) of 8-byte units; the whole pool is ~2n
     // bytes: a unit for every 4 input bytes covers every token missing the LDS table even on
@@ -1080,7 +1123,8 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // take ~25 us and could not run beside k_agg anyway (its workgroups fill every CU's LDS),
     // while the fork and join cost ~25 us of dependency latency.
     const bool long_path = ablate == 0 || ablate >= 6;
-    const bool fork = long_path && two_pass;
+    static const char* fork_env = getenv("WCG_LONG_FORK");     // diagnostics: 0 = in line (alone)
+    const bool fork = long_path && two_pass && !(fork_env && atoi(fork_env) == 0);
     hipStream_t ls = fork ? c->long_stream : c->stream;
     if (fork) {
         HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
@@ -1097,7 +1141,12 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         if (c->lpcur != old_cur) HIPCHK(c, hipMemsetAsync(c->lpcur, 0, LQ * sizeof(u32), ls));
         lp.ent = c->lent; lp.cur = c->lpcur;
         k_long_hash<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, ls>>>(a, lp, (u32)grid);
-        k_long_agg<<<LQ, LONG_NT, 0, ls>>>(a, lp);
+#ifndef WCG_LA_PERSIST
+#define WCG_LA_PERSIST 1
+#endif
+        static_assert(LQ / LA_MAXQ <= 256, "k_long_agg's grid covers every partition");
+        k_long_agg<<<(unsigned)(WCG_LA_PERSIST ? std::max<u64>(std::min<u64>(LQ, c->ncu), LQ / LA_MAXQ) : LQ), LA_NT,
+                     0, ls>>>(a, lp);
         HIPCHK(c, hipGetLastError());
         if (fork) HIPCHK(c, hipEventRecord(c->ev_join, c->long_stream));
     }

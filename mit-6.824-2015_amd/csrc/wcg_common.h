@@ -75,6 +75,8 @@ constexpr u64 ST_SCALAR_OFF = 128;   // the scalars follow DevState in one alloc
 constexpr u64 ST_TIE_GROUPS = 16;    // scalar slot of the tie-group count (the scans use 0, the sort 8)
 constexpr u64 ST_GLIST = 24;         // scalar slot: two-pass contexts' global-table claim list, or 0
 constexpr u64 GLIST_CAP = 1ull << 20;   // claims listed (more: compaction and reset scan it all)
+constexpr u64 ST_LLIST = 25;         // scalar slot: large contexts' long-key-table claim list, or 0
+constexpr u64 LLIST_CAP = 1ull << 22;   // (C4 1 GiB: 1.6M long keys in a 16M-slot, 512 MiB table)
 struct DevState {
     u64 tokens;          // tokens seen by map kernels
     u64 lds_hits;        // tokens aggregated in LDS
@@ -85,10 +87,13 @@ struct DevState {
     u64 nlong;           // ... of which long keys (> 15 bytes)
     u64 nemit;           // records emitted by k_agg's pass 2 (the record log, across map calls)
     u64 gnew;            // global-table slots claimed since wcg_reset (two-pass contexts list them)
+    u64 lnew;            // long-key-table slots claimed since wcg_reset (large contexts list them)
+    u64 lemit;           // long-key records k_long_agg put in the record log (two-pass jobs)
+    u64 lheap_top;       // bytes of those records' keys in the log heap (after the table's heap)
     u32 overflow;        // table / arena full -> WCG_EFULL
     u32 spin_fail;       // bounded spin gave up -> WCG_EFULL (never expected)
     u32 bad_input;       // malformed record units (wcg_import) or lines (wcg_merge_runs) -> WCG_EINVAL
-    u32 pad_;
+    u32 long_fb;         // diagnostics: long-key entries counted by a fenced table insert (fallbacks)
 };
 
 // ------------------------------------------------------------------ letters
@@ -339,6 +344,14 @@ __device__ __host__ __forceinline__ u64 mix64(u64 x) {
     x ^= x >> 32; x *= 0xD6E8FEB86659FD93ull; x ^= x >> 32; x *= 0xD6E8FEB86659FD93ull; x ^= x >> 32;
     return x;
 }
+
+// Long keys (> 15 bytes) are tagged by a hash of their bytes taken a little-endian 32-bit word at a
+// time (zeros past the key's end), finished by mix64 with the length: every kernel that tags a
+// long key (k_long_hash / k_long_agg / k_import) must use these.  Internal only - the partition
+// hash of the reference (ihash, FNV-1a 32) is computed separately.  (r04: it was FNV-1a 64 byte by
+// byte, ~5 VALU per byte on the hashing lane.)
+__device__ __forceinline__ u64 lhash_step(u64 h, u32 w) { return (h ^ w) * 0x100000001B3ull; }
+constexpr u64 LHASH_INIT = 0xCBF29CE484222325ull;
 // 64-bit key hash: miss-log bucket and global-table slot (computed off the hit path)
 __device__ __forceinline__ u64 key_hash(u64 k0, u64 k1) {
     return mix64(k0 * 0x9E3779B97F4A7C15ull + (k1 ^ (k1 >> 29)) * 0xC2B2AE3D27D4EB4Full);
@@ -403,6 +416,18 @@ __device__ __forceinline__ void add_agent(u64* p, u64 v) {
 
 constexpr int SPIN_LIMIT = 1 << 20;
 
+// a table slot just claimed by this thread, appended to the context's claim list when it keeps one
+// (scalar slot `which` of DevState's block): compaction and wcg_reset then visit the listed slots
+// instead of the whole table; past `cap` claims they scan it all
+__device__ __forceinline__ void list_claim(DevState* st, u64 which, u64* counter, u64 cap, u64 s) {
+    u64* const l = *reinterpret_cast<u64* const*>(reinterpret_cast<const uint8_t*>(st) + ST_SCALAR_OFF +
+                                                  which * sizeof(u64));
+    if (l) {
+        const u64 i = atomicAdd((unsigned long long*)counter, 1ull);
+        if (i < cap) l[i] = s;
+    }
+}
+
 // Insert/accumulate an inline key into the global table (open addressing, linear probing from
 // slot_hash).  Claim protocol: CAS k0 0 -> key; a key of 8+ bytes then publishes k1 (never 0).
 // A reader that sees k0 == key but k1 == 0 re-reads in a later iteration (the claimer publishes
@@ -423,12 +448,7 @@ __device__ __forceinline__ void ginsert(GEntry* tab, u64 mask, u64 k0, u64 k1, u
                 // two-pass contexts keep the global table nearly empty (a few fallback inserts per
                 // GiB) and list its claimed slots, so that compaction and wcg_reset visit those
                 // slots instead of the whole (GB-sized) table
-                u64* const gl = *reinterpret_cast<u64* const*>(reinterpret_cast<const uint8_t*>(st) + ST_SCALAR_OFF +
-                                                               ST_GLIST * sizeof(u64));
-                if (gl) {
-                    const u64 i = atomicAdd((unsigned long long*)&st->gnew, 1ull);
-                    if (i < GLIST_CAP) gl[i] = s;
-                }
+                list_claim(st, ST_GLIST, &st->gnew, GLIST_CAP, s);
                 return;
             }
             c0 = exp;

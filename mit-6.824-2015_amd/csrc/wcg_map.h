@@ -100,6 +100,7 @@ struct MapArgs {
     GEntry* gtab;  u64 gmask;      // inline-key table
     GEntry* ltab;  u64 lmask;      // long-key table
     uint8_t* arena; u64 arena_cap;
+    u64 lheap_cap;                 // two-pass contexts: the log heap after the table's heap (bytes)
     DevState* st;
     u64* pool;     u64 region_cap;  // miss log: region (wg, p) = pool[(wg * P + p) * region_cap ...]
     u32* region_len;               // units written per region
@@ -174,6 +175,7 @@ __device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 tag, W w,
         if (c0 == 0) {
             u64 exp = 0;
             if (cas_agent(&e->k0, &exp, tag)) {
+                list_claim(a.st, ST_LLIST, &a.st->lnew, LLIST_CAP, s);
                 const u64 off = long_home(s, len, a.lmask + 1, a.arena_cap, &a.st->arena_top);
                 if (off == ~0ull) { atomicAdd(&a.st->overflow, 1u); return 0; }
                 const u64 cells = long_cells(len);
@@ -218,22 +220,51 @@ __device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 tag, W w,
     }
 }
 
-// length of the letter run at absolute offset p (walking runes in global memory), its FNV-1a 64
-__device__ u64 long_walk(const MapArgs& a, u64 p, u64* hash) {
-    const uint8_t* in = a.in;
+// aligned input dword at byte offset off (a multiple of 4); bytes past the input read as 0
+__device__ __forceinline__ u32 input_dword(const MapArgs& a, u64 off) {
+    if (off + 4 <= a.n) return *reinterpret_cast<const u32*>(a.in + off);
+    u32 v = 0;
+    for (u32 b = 0; b < 4; b++) if (off + b < a.n) v |= (u32)a.in[off + b] << (8 * b);
+    return v;
+}
+
+// length of the letter run at absolute offset p (a run that reached the map window's look-ahead
+// chunk).  16-byte chunks are loaded whole (one round trip each): an all-ASCII chunk is classified
+// by the SWAR mask, any other one rune by rune from its registers (r04: the byte-at-a-time walk
+// waited on a global load per byte - C4's walked runs cost k_long_hash most of its 0.9-1.3 ms)
+__device__ u64 long_walk(const MapArgs& a, u64 p) {
     const u64 n = a.n;
-    auto at = [&](long i) -> u32 { return (i >= 0 && (u64)i < n) ? in[i] : 0u; };
     u64 q = p;
-    u64 h = 0xCBF29CE484222325ull;
     while (q < n) {
-        u32 cp;
-        int w = go_decode(at, (long)q, &cp);
-        if (w == 0 || !lt_is_letter(cp)) break;
-        for (int k = 0; k < w; k++) { h ^= in[q + k]; h *= 0x100000001B3ull; }
-        q += w;
+        const u64 base = q & ~15ull;
+        const uint4 c = load_chunk(a.in, n, (long)base);
+        const u32 off = (u32)(q - base);
+        if (all_ascii(c)) {
+            const u32 m = ascii_mask16(c) >> off;
+            const u32 run = (u32)__builtin_ctz(~m);          // letters from q within the chunk
+            q += run;
+            if (run < 16 - off) return q - p;
+            continue;
+        }
+        const u32 d4 = input_dword(a, base + 16);           // runes may end up to 3 bytes past
+        const u32 d[5] = {c.x, c.y, c.z, c.w, d4};
+        auto at = [&](long i) -> u32 {                       // chunk byte i (0..19); 0 past the input
+            if ((u64)(base + i) >= n) return 0u;
+            u32 w = 0;                                       // masks, not selects (no indexed array)
+#pragma unroll
+            for (int k = 0; k < 5; k++) w |= d[k] & (0u - (u32)((i >> 2) == k));
+            return (w >> (8 * (i & 3))) & 0xFFu;
+        };
+        u32 j = off;
+        while (j < 16) {
+            u32 cp;
+            const int w = go_decode(at, (long)j, &cp);
+            if (w == 0 || !lt_is_letter(cp)) return base + j - p;
+            j += (u32)w;
+        }
+        q = base + j;
     }
-    *hash = h;
-    return q - p;
+    return n - p;
 }
 
 // a run that turned out to be an inline key (<= 15 bytes: measured only after a rune walk); called
@@ -275,13 +306,6 @@ __device__ __forceinline__ u32 input_word(const MapArgs& a, u64 p, u32 len, u64 
     return rem >= 4 ? v : v & ((1u << (8 * rem)) - 1);
 }
 
-// aligned input dword at byte offset off (a multiple of 4); bytes past the input read as 0
-__device__ __forceinline__ u32 input_dword(const MapArgs& a, u64 off) {
-    if (off + 4 <= a.n) return *reinterpret_cast<const u32*>(a.in + off);
-    u32 v = 0;
-    for (u32 b = 0; b < 4; b++) if (off + b < a.n) v |= (u32)a.in[off + b] << (8 * b);
-    return v;
-}
 
 // key words j0 .. j0+7 of the key at input offset p (len bytes; zeros past len), from 9 aligned
 // dword loads issued together: a word-at-a-time loop waits for each load in turn, and these
@@ -300,17 +324,18 @@ __device__ __forceinline__ void input_words8(const MapArgs& a, u64 p, u32 len, u
     }
 }
 
-// FNV-1a 64 of the long key at input offset p (len bytes)
-__device__ __forceinline__ u64 input_fnv64(const MapArgs& a, u64 p, u32 len) {
-    u64 h = 0xCBF29CE484222325ull;
+// the long-key hash (lhash_step) of the key at input offset p (len bytes), and its first 8 words
+// (key bytes 0-31, zeros past len) in w8
+__device__ __forceinline__ u64 input_lhash(const MapArgs& a, u64 p, u32 len, u32 (&w8)[8]) {
+    u64 h = LHASH_INIT;
     for (u32 j0 = 0; 4 * j0 < len; j0 += 8) {
         u32 v[8];
         input_words8(a, p, len, j0, v);
 #pragma unroll
-        for (int k = 0; k < 8; k++)
-#pragma unroll
-            for (int b = 0; b < 4; b++)
-                if (4 * (j0 + k) + b < len) { h ^= (v[k] >> (8 * b)) & 0xFFu; h *= 0x100000001B3ull; }
+        for (int k = 0; k < 8; k++) {
+            if (j0 == 0) w8[k] = v[k];
+            if (4 * (j0 + k) < len) h = lhash_step(h, v[k]);
+        }
     }
     return h;
 }
@@ -360,25 +385,68 @@ __device__ __forceinline__ void long_token_log(const MapArgs& a, u64 p, u32 rp, 
 //      adds the key to the long-key table once, unfenced.  The per-occurrence table inserts of a
 //      flat design serialise on hot keys and on the fences that publish arena bytes across CUs.
 constexpr u32 LQ = 2048;                      // partitions
-struct LEnt { u64 h; u64 rec; u64 cnt; };     // FNV-1a 64, input offset | len << 40, occurrences
+// an entry: lhash, input offset | len << 40, occurrences, and the key's bytes 0-31 (zeros past
+// len), so that k_long_agg compares keys of up to 32 bytes (C4: nearly all long keys) in LDS
+// instead of re-reading two occurrences from the input (r04)
+struct LEnt { u64 h; u64 rec; u64 cnt; u64 pad; uint4 w0, w1; };
+static_assert(sizeof(LEnt) == 64, "four 16-byte stores per entry");
 struct LongPart { LEnt* ent; u32* cur; u32 cap; };
 __device__ __forceinline__ u32 long_part(u64 tag) { return (u32)(tag >> 40) & (LQ - 1); }
+__device__ __forceinline__ bool w8_same(const u32 (&x)[8], const uint4& y0, const uint4& y1) {
+    return ((x[0] ^ y0.x) | (x[1] ^ y0.y) | (x[2] ^ y0.z) | (x[3] ^ y0.w) | (x[4] ^ y1.x) | (x[5] ^ y1.y) |
+            (x[6] ^ y1.z) | (x[7] ^ y1.w)) == 0;
+}
+// the words of a long key for ltab_add: words 0-7 (bytes 0-31, zeros past len) held here, the rest
+// read from the input at offset p.  A plain struct (no reference to the kernel's arguments and no
+// array indexed at run time: either put the whole argument block or the array in scratch)
+struct LongKeyWords {
+    const uint8_t* in; u64 n; u64 p; u32 len; u32 w[8];
+    __device__ __forceinline__ u32 operator()(u64 j) const {
+        if (j >= 8) {
+            if (4 * (u32)j >= len) return 0u;
+            u32 v = 0;
+            for (u32 b = 0; b < 4 && 4 * (u32)j + b < len; b++) v |= (u32)in[p + 4 * j + b] << (8 * b);
+            return v;
+        }
+        u32 r = 0;                    // masks, not selects (selects fold back into an indexed load)
+#pragma unroll
+        for (int k = 0; k < 8; k++) r |= w[k] & (0u - (u32)(j == (u64)k));
+        return r;
+    }
+};
+__device__ __forceinline__ LongKeyWords long_words(const MapArgs& a, u64 p, u64 len, const u32 (&w)[8]) {
+    LongKeyWords k;
+    k.in = a.in; k.n = a.n; k.p = p; k.len = (u32)len;
+#pragma unroll
+    for (int i = 0; i < 8; i++) k.w[i] = w[i];
+    return k;
+}
+// the same long key (len bytes each) at input offsets p and q, whose bytes 0-31 are known equal
+__device__ __forceinline__ bool long_rest_same(const MapArgs& a, u64 p, u64 q, u32 len) {
+    return len <= 32 || input_same(a, p + 32, q + 32, len - 32);
+}
 
 // k_long_hash: workgroup b reads map region b % nreg (its LONG_PARTS workgroups stride over the
 // region's records in rounds of LONG_NT), hashes each logged token from the resident input
-// (walking runes for records of length 0) and emits {h, rec, count} to the token's partition.
-// Repeats are pre-aggregated in an LDS cache keyed by tag (hot keys: C4's top long key occurs
-// 1.2e5 times per GiB), compared byte-exactly against the cached occurrence's input bytes - no
-// other CU's writes are read, so no fence is needed.  A lane never waits on another's LDS write:
-// a cache entry claimed in the same round may still have no representative (rec 0), and such a
-// lane simply emits its own entry.  A full partition falls back to a fenced table insert.
+// (walking runes for records of length 0) and emits {h, rec, count, bytes 0-31} to the token's
+// partition.  Repeats are pre-aggregated in an LDS cache keyed by tag (hot keys: C4's top long key
+// occurs 1.2e5 times per GiB), compared byte-exactly against the cached representative's bytes
+// (LDS; bytes past 32 from the input) - no other CU's writes are read, so no fence is needed.  A
+// lane never waits on another's LDS write: a cache entry claimed in the same round may still have
+// no representative (rec 0), and such a lane simply emits its own entry.  A full partition falls
+// back to a fenced table insert.
 constexpr int LONG_NT = 256;
 constexpr int LONG_PARTS = 8;
-constexpr int LCACHE = 1024;                  // LDS cache entries (20 B each)
+#ifndef WCG_LCACHE
+#define WCG_LCACHE 512
+#endif
+constexpr int LCACHE = WCG_LCACHE;            // LDS cache entries (60 B each: 512 -> 5 workgroups per CU)
 __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u32 nreg) {
     __shared__ u64 ctag[LCACHE];
     __shared__ u64 crec[LCACHE];              // representative occurrence (0 = not yet set)
+    __shared__ u64 chash[LCACHE];
     __shared__ u32 ccnt[LCACHE];
+    __shared__ uint4 cw[LCACHE][2];           // representative's bytes 0-31
     const u32 reg = blockIdx.x % nreg, part = blockIdx.x / nreg;
     const u32 nrec = a.llog_len[reg];
     const u64* recs = a.llog + (u64)reg * a.llog_cap;
@@ -387,15 +455,20 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
     if (rounds == 0) return;          // ASCII text: nearly every workgroup (no barrier reached yet)
     for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; crec[e] = 0; ccnt[e] = 0; }
     __syncthreads();
-    auto emit = [&](u64 h, u64 rec, u64 c) {
+    auto emit = [&](u64 h, u64 rec, u64 c, const u32 (&w)[8]) {
         const u64 len = rec >> 40, p = rec & LLOG_OFF_MASK;
-        const u32 q = long_part(long_tag(h, len));
+        const u64 tag = long_tag(h, len);
+        const u32 q = long_part(tag);
         const u32 pos = atomicAdd(&lp.cur[q], 1u);
         if (pos < lp.cap) {
-            LEnt* d = lp.ent + (u64)q * lp.cap + pos;
-            d->h = h; d->rec = rec; d->cnt = c;
+            uint4* d = reinterpret_cast<uint4*>(lp.ent + (u64)q * lp.cap + pos);
+            d[0] = make_uint4((u32)h, (u32)(h >> 32), (u32)rec, (u32)(rec >> 32));
+            d[1] = make_uint4((u32)c, (u32)(c >> 32), 0u, 0u);
+            d[2] = make_uint4(w[0], w[1], w[2], w[3]);
+            d[3] = make_uint4(w[4], w[5], w[6], w[7]);
         } else {                      // partition full: count it here (fenced, exact)
-            ltab_add(a, len, long_tag(h, len), [&](u64 j) -> u32 { return input_word(a, p, (u32)len, j); }, c, true);
+            atomicAdd(&a.st->long_fb, 1u);
+            ltab_add(a, len, tag, long_words(a, p, len, w), c, true);
         }
     };
     for (u32 k = 0; k < rounds; k++) {
@@ -403,13 +476,13 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
         const u64 r = i < nrec ? recs[i] : 0;
         const u64 p = r & LLOG_OFF_MASK;
         u64 len = r >> 40, h = 0;
+        u32 w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (i < nrec && len == 0) {
-            len = long_walk(a, p, &h);
+            len = long_walk(a, p);
             if (len <= 15) { count_inline_run(a, p, len); len = 0; }
             else if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); len = 0; }
-        } else if (len != 0) {
-            h = input_fnv64(a, p, (u32)len);
         }
+        if (len != 0) h = input_lhash(a, p, (u32)len, w);
         if (len != 0) {
             const u64 tag = long_tag(h, len), rec = p | len << 40;
             const u32 c0 = (u32)(tag >> 24) & (LCACHE - 1);
@@ -419,50 +492,88 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
                 u64 t = ctag[cs];
                 if (t == 0) {
                     t = atomicCAS((unsigned long long*)&ctag[cs], 0ull, (unsigned long long)tag);
-                    if (t == 0) { crec[cs] = rec; atomicAdd(&ccnt[cs], 1u); done = true; break; }
+                    if (t == 0) {
+                        cw[cs][0] = make_uint4(w[0], w[1], w[2], w[3]);
+                        cw[cs][1] = make_uint4(w[4], w[5], w[6], w[7]);
+                        chash[cs] = h;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        __hip_atomic_store(&crec[cs], rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        atomicAdd(&ccnt[cs], 1u);
+                        done = true;
+                        break;
+                    }
                 }
                 if (t != tag) continue;
-                const u64 rr = crec[cs];
-                if (rr != 0 && (rr >> 40) == len && input_same(a, p, rr & LLOG_OFF_MASK, (u32)len)) {
-                    atomicAdd(&ccnt[cs], 1u);
-                    done = true;
+                const u64 rr = __hip_atomic_load(&crec[cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (rr != 0 && (rr >> 40) == len) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    if (w8_same(w, cw[cs][0], cw[cs][1]) && long_rest_same(a, p, rr & LLOG_OFF_MASK, (u32)len)) {
+                        atomicAdd(&ccnt[cs], 1u);
+                        done = true;
+                    }
                 }
                 break;                // same tag, other key or not yet set: emit
             }
-            if (!done) emit(h, rec, 1);
+            if (!done) emit(h, rec, 1, w);
         }
         __syncthreads();              // this round's representatives are visible to the next
     }
     for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) {
         const u64 rr = crec[e];
         if (rr == 0 || ccnt[e] == 0) continue;
-        const u64 len = rr >> 40, p = rr & LLOG_OFF_MASK;
-        emit(input_fnv64(a, p, (u32)len), rr, ccnt[e]);
+        const uint4 x = cw[e][0], y = cw[e][1];
+        const u32 w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        emit(chash[e], rr, ccnt[e], w);
     }
 }
 
-// k_long_agg: one workgroup per partition.  Rounds of LONG_NT entries: (1) each entry claims or
-// finds its tag's LDS slot (linear probing) and the claimer stores its occurrence as the slot's
-// representative; barrier; (2) each entry compares its bytes with the representative's and adds
-// its count.  A tag collision between different keys, or a full table, falls back to a fenced
-// table insert of that entry (exact).  Finally every slot is added to the long-key table once.
+// k_long_agg: one workgroup per partition.  Rounds of LA_NT entries: (1) each entry claims or
+// finds its tag's LDS slot (linear probing) and the claimer stores its key bytes 0-31 and
+// occurrence as the slot's representative; barrier; (2) each entry compares its bytes with the
+// representative's (LDS; bytes past 32 from the input) and adds its count.  A tag collision
+// between different keys, or a full table, falls back to a fenced table insert of that entry
+// (exact).  Finally every slot is added to the long-key table once, from its LDS bytes.
+#ifndef WCG_LA_ABL
+#define WCG_LA_ABL 0                          // diagnostics (wrong counts): 1 = no table inserts, 2 = no fallbacks
+#endif
 constexpr u32 LA_SLOTS = 2048;
 constexpr u32 LA_PROBES = 32;
-__global__ __launch_bounds__(LONG_NT) void k_long_agg(MapArgs a, LongPart lp) {
-    __shared__ u64 stag[LA_SLOTS], srec[LA_SLOTS], scnt[LA_SLOTS], sh[LA_SLOTS];
-    const u32 q = blockIdx.x;
-    const u32 nq = lp.cur[q] < lp.cap ? lp.cur[q] : lp.cap;
-    if (nq == 0) return;
-    for (u32 s = threadIdx.x; s < LA_SLOTS; s += LONG_NT) { stag[s] = 0; srec[s] = 0; scnt[s] = 0; }
+constexpr int LA_NT = 512;                    // one 112 KiB workgroup per CU: 8 waves
+constexpr u32 LA_MAXQ = 64;                   // partitions per workgroup (grid >= LQ / LA_MAXQ)
+// A persistent grid over the LQ partitions (one 112 KiB workgroup per CU; on low-cardinality
+// text nearly every partition is empty and costs one read of its cursor, not a launch slot)
+__global__ __launch_bounds__(LA_NT) void k_long_agg(MapArgs a, LongPart lp) {
+    __shared__ u64 stag[LA_SLOTS], srec[LA_SLOTS], scnt[LA_SLOTS];
+    __shared__ uint4 sw[LA_SLOTS][2];
+    __shared__ u32 qn[LA_MAXQ];               // this workgroup's partitions' entry counts
+    __shared__ u32 la_wk[LA_NT / 64], la_wb[LA_NT / 64];   // per-wave key / heap byte sums
+    __shared__ u64 la_base[2];                // the partition's record-log and heap reservations
+    // every cursor of the workgroup's partitions read at once (one round trip, not one per
+    // partition), then reset for the next map call
+    for (u32 t = threadIdx.x, q = blockIdx.x + t * gridDim.x; t < LA_MAXQ; t += LA_NT, q += LA_NT * gridDim.x) {
+        const u32 cq = q < LQ ? lp.cur[q] : 0u;
+        qn[t] = cq;
+        if (cq) lp.cur[q] = 0;
+    }
+    __syncthreads();
+    for (u32 t = 0, q = blockIdx.x; q < LQ; t++, q += gridDim.x) {
+    const u32 nq = qn[t] < lp.cap ? qn[t] : lp.cap;
+    if (nq == 0) continue;
+    for (u32 s = threadIdx.x; s < LA_SLOTS; s += LA_NT) { stag[s] = 0; srec[s] = 0; scnt[s] = 0; }
     __syncthreads();
     const LEnt* E = lp.ent + (u64)q * lp.cap;
-    for (u32 base = 0; base < nq; base += LONG_NT) {
+    for (u32 base = 0; base < nq; base += LA_NT) {
         const u32 e = base + threadIdx.x;
         const bool valid = e < nq;
-        LEnt x = {0, 0, 0};
-        if (valid) x = E[e];
-        const u64 len = x.rec >> 40, p = x.rec & LLOG_OFF_MASK;
-        const u64 tag = long_tag(x.h, len);
+        uint4 d0 = make_uint4(0, 0, 0, 0), d1 = d0, d2 = d0, d3 = d0;
+        if (valid) {
+            const uint4* src = reinterpret_cast<const uint4*>(E + e);
+            d0 = src[0]; d1 = src[1]; d2 = src[2]; d3 = src[3];
+        }
+        const u64 h = (u64)d0.y << 32 | d0.x, rec = (u64)d0.w << 32 | d0.z, cnt = (u64)d1.y << 32 | d1.x;
+        const u32 w[8] = {d2.x, d2.y, d2.z, d2.w, d3.x, d3.y, d3.z, d3.w};
+        const u64 len = rec >> 40, p = rec & LLOG_OFF_MASK;
+        const u64 tag = long_tag(h, len);
         int slot = -1;
         if (valid) {
             const u32 s0 = (u32)(tag >> 8) & (LA_SLOTS - 1);
@@ -471,7 +582,7 @@ __global__ __launch_bounds__(LONG_NT) void k_long_agg(MapArgs a, LongPart lp) {
                 u64 t = stag[s];
                 if (t == 0) {
                     t = atomicCAS((unsigned long long*)&stag[s], 0ull, (unsigned long long)tag);
-                    if (t == 0) { srec[s] = x.rec; sh[s] = x.h; slot = (int)s; break; }
+                    if (t == 0) { srec[s] = rec; sw[s][0] = d2; sw[s][1] = d3; slot = (int)s; break; }
                 }
                 if (t == tag) { slot = (int)s; break; }
             }
@@ -480,20 +591,100 @@ __global__ __launch_bounds__(LONG_NT) void k_long_agg(MapArgs a, LongPart lp) {
         bool fallback = valid && slot < 0;
         if (valid && slot >= 0) {
             const u64 rr = srec[slot];
-            if ((rr >> 40) == len && input_same(a, p, rr & LLOG_OFF_MASK, (u32)len)) atomicAdd((unsigned long long*)&scnt[slot], (unsigned long long)x.cnt);
+            if ((rr >> 40) == len && w8_same(w, sw[slot][0], sw[slot][1]) &&
+                long_rest_same(a, p, rr & LLOG_OFF_MASK, (u32)len))
+                atomicAdd((unsigned long long*)&scnt[slot], (unsigned long long)cnt);
             else fallback = true;
         }
-        if (fallback)
-            ltab_add(a, len, tag, [&](u64 j) -> u32 { return input_word(a, p, (u32)len, j); }, x.cnt, true);
+        if (fallback && !(WCG_LA_ABL & 2)) {
+            atomicAdd(&a.st->long_fb, 1u);
+            ltab_add(a, len, tag, long_words(a, p, len, w), cnt, true);
+        }
         __syncthreads();              // slots claimed in the next round cannot be confused with ...
     }                                 // ... representatives read in this one
-    for (u32 s = threadIdx.x; s < LA_SLOTS; s += LONG_NT) {
+    // Two-pass jobs (a record log): the partition's keys become records of the log directly, their
+    // bytes copied to the arena heap - one reservation of log records and one of heap bytes per
+    // partition.  (r04: adding them to the long-key table took 1.4 of the kernel's 1.6 ms on C4:
+    // 1.6M dependent probe / claim / publish chains over a 512 MiB table.)  A key repeated by
+    // another map call, or also counted through the table (fallbacks, imports), is merged after
+    // the sort (k_tie_sort).  Otherwise, or when the log or the heap is full: the table, once.
+    bool to_log = a.emit != nullptr && a.lheap_cap != 0 && !(WCG_LA_ABL & 1);
+    u32 rk[LA_SLOTS / LA_NT];                 // this thread's slots: rank among filled ones, heap bytes
+    u32 hb[LA_SLOTS / LA_NT];
+    if (to_log) {
+        // slots t * LA_NT + tid: per-thread counts, then a block prefix sum (waves in order)
+        u32 nk = 0, nb = 0;
+#pragma unroll
+        for (u32 k = 0; k < LA_SLOTS / LA_NT; k++) {
+            const u32 sl = k * LA_NT + threadIdx.x;
+            const bool f = scnt[sl] != 0;
+            rk[k] = nk; hb[k] = nb;
+            nk += f ? 1u : 0u;
+            nb += f ? (u32)long_cells(srec[sl] >> 40) : 0u;
+        }
+        const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        u32 ik = nk, ib = nb;
+        for (int d = 1; d < 64; d <<= 1) {
+            const u32 yk = __shfl_up(ik, d, 64), yb = __shfl_up(ib, d, 64);
+            if (lane >= (u32)d) { ik += yk; ib += yb; }
+        }
+        if (lane == 63) { la_wk[wv] = ik; la_wb[wv] = ib; }
+        __syncthreads();
+        u32 pk = 0, pb = 0, tk = 0, tb = 0;
+        for (u32 v = 0; v < LA_NT / 64; v++) {
+            if (v < wv) { pk += la_wk[v]; pb += la_wb[v]; }
+            tk += la_wk[v]; tb += la_wb[v];
+        }
+        if (threadIdx.x == 0) {
+            // log-heap bytes first (a heap of their own: a reservation past its cap leaves the
+            // table's heap untouched; r04: a CAS loop on the shared top serialised the 256
+            // workgroups, ~1.5 ms), then the log records; nothing once the log is full
+            u64 h0 = ~0ull, r0 = ~0ull;
+            if (tk && ld_agent(&a.st->nemit) < a.emit_cap) {
+                const u64 h = atomicAdd((unsigned long long*)&a.st->lheap_top, (unsigned long long)tb);
+                if (h + tb <= a.lheap_cap) {
+                    h0 = h;
+                    r0 = atomicAdd((unsigned long long*)&a.st->nemit, (unsigned long long)tk);
+                }
+            }
+            la_base[0] = r0;
+            la_base[1] = h0;
+            // keys past the log's cap go to the table (their heap bytes stay unused)
+            const u64 fit = r0 == ~0ull || r0 >= a.emit_cap ? 0 : (a.emit_cap - r0 < tk ? a.emit_cap - r0 : tk);
+            if (fit) atomicAdd((unsigned long long*)&a.st->lemit, (unsigned long long)fit);
+        }
+        __syncthreads();
+        to_log = la_base[0] != ~0ull;
+#pragma unroll
+        for (u32 k = 0; k < LA_SLOTS / LA_NT; k++) { rk[k] += pk + ik - nk; hb[k] += pb + ib - nb; }
+    }
+#pragma unroll
+    for (u32 k = 0; k < LA_SLOTS / LA_NT; k++) {
+        const u32 s = k * LA_NT + threadIdx.x;
         const u64 c = scnt[s];
         if (c == 0) continue;
         const u64 rr = srec[s], len = rr >> 40, p = rr & LLOG_OFF_MASK;
-        ltab_add(a, len, long_tag(sh[s], len), [&](u64 j) -> u32 { return input_word(a, p, (u32)len, j); }, c, false);
+        const uint4 x = sw[s][0], y = sw[s][1];
+        const u32 w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        if (to_log && la_base[0] + rk[k] < a.emit_cap) {
+            const u64 off = (a.lmask + 1) * LONG_CELL + a.arena_cap + la_base[1] + hb[k];
+            const LongKeyWords kw = long_words(a, p, len, w);
+            const u64 cells = long_cells(len);
+            for (u64 j = 0; j < cells; j += 16)
+                *reinterpret_cast<uint4*>(a.arena + off + j) =
+                    make_uint4(kw(j / 4), kw(j / 4 + 1), kw(j / 4 + 2), kw(j / 4 + 3));
+            Rec r;
+            r.hi = bswap64((u64)x.y << 32 | x.x);
+            r.lo = bswap64((u64)x.w << 32 | x.z);
+            r.cnt = c;
+            r.ref = LONG_FLAG | (len << 40) | off;
+            a.emit[la_base[0] + rk[k]] = r;
+        } else if (!(WCG_LA_ABL & 1)) {
+            ltab_add(a, len, stag[s], long_words(a, p, len, w), c, false);
+        }
     }
-    if (threadIdx.x == 0) lp.cur[q] = 0;      // for the next map call (every thread read it long ago)
+    __syncthreads();                          // the LDS is reused by the next partition
+    }
 }
 
 // wave-local ordering of LDS accesses between lanes (the LDS executes one wave's

@@ -22,10 +22,11 @@ constexpr int CP_NT = 256, CP_IPT = 8;          // 2048 table slots per block, o
 
 // Each thread takes CP_IPT slots: every slot entry is loaded first, unconditionally (a load in a
 // per-slot branch made a serial chain of memory latencies), then long keys' 16-byte prefixes.
-// glist (two-pass jobs): the gtab part is the gslots listed slots gtab[glist[i]], not gtab[0, gslots)
+// glist (two-pass jobs): the gtab part is the gslots listed slots gtab[glist[i]], not gtab[0, gslots);
+// llist (large contexts): the ltab part is the lslots listed slots ltab[llist[i]]
 __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
                                                   const uint8_t* arena, Rec* out, u64 cap, DevState* st, u64* zero,
-                                                  const u64* glist) {
+                                                  const u64* glist, const u64* llist = nullptr) {
     if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;   // a later kernel's counter
     __shared__ u32 wsum[CP_NT / 64], wlong[CP_NT / 64];
     __shared__ u64 base_s;
@@ -40,7 +41,9 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
 #pragma unroll
     for (int j = 0; j < CP_IPT; j++) {
         const u64 i = b0 + (u64)j * CP_NT + tid;
-        const GEntry* src = i < gslots ? gtab + (glist ? glist[i] : i) : ltab + (i < total ? i - gslots : lslots - 1);
+        // (past the end: slot 0 of ltab, a valid address whose entry is then ignored)
+        const u64 li = i < total ? i - gslots : 0;
+        const GEntry* src = i < gslots ? gtab + (glist ? glist[i] : i) : ltab + (llist && i < total ? llist[li] : li);
         e[j] = *src;
         if (i >= total) e[j].k0 = 0;
     }
@@ -96,11 +99,14 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
 
 // wcg_reset: zero n1 + n2 16-byte words of two tables and the DevState counters, one dispatch;
 // with list1 the first table's part is the n1 / 2 listed 32-byte entries t1[2 list1[i] + {0, 1}]
-__global__ void k_clear(uint4* t1, u64 n1, uint4* t2, u64 n2, DevState* st, const u64* list1) {
+// (list2: the same for the second table)
+__global__ void k_clear(uint4* t1, u64 n1, uint4* t2, u64 n2, DevState* st, const u64* list1, const u64* list2) {
     const uint4 z = make_uint4(0, 0, 0, 0);
     const u64 stride = (u64)gridDim.x * blockDim.x;
     for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i < n1 + n2; i += stride) {
-        if (i < n1) t1[list1 ? 2 * list1[i >> 1] + (i & 1) : i] = z; else t2[i - n1] = z;
+        const u64 j = i - n1;
+        if (i < n1) t1[list1 ? 2 * list1[i >> 1] + (i & 1) : i] = z;
+        else t2[list2 ? 2 * list2[j >> 1] + (j & 1) : j] = z;
     }
     if (blockIdx.x == 0) {
         u32* w = reinterpret_cast<u32*>(st);
@@ -619,8 +625,12 @@ __global__ void k_import(const Rec* in, u64 n, GEntry* gtab, u64 gmask, GEntry* 
         u64 len = (x.ref >> 40) & LONG_LEN_MAX;
         const Rec* src = in + i + 1;
         if (i + 1 + (len + CONT_BYTES - 1) / CONT_BYTES > n) { atomicAdd(&st->overflow, 1u); continue; }
-        u64 h = 0xCBF29CE484222325ull;
-        for (u64 k = 0; k < len; k++) { h ^= cont_byte(src, k); h *= 0x100000001B3ull; }
+        u64 h = LHASH_INIT;
+        for (u64 k = 0; k < len; k += 4) {
+            u32 w = 0;
+            for (u64 b = 0; b < 4 && k + b < len; b++) w |= (u32)cont_byte(src, k + b) << (8 * b);
+            h = lhash_step(h, w);
+        }
         u64 tag = mix64(h ^ len) | 1ull;
         u64 s = tag & lmask, probes = 0;
         int spins = 0;
@@ -630,6 +640,7 @@ __global__ void k_import(const Rec* in, u64 n, GEntry* gtab, u64 gmask, GEntry* 
             if (c0 == 0) {
                 u64 exp = 0;
                 if (cas_agent(&e->k0, &exp, tag)) {
+                    list_claim(st, ST_LLIST, &st->lnew, LLIST_CAP, s);
                     const u64 off = long_home(s, len, lmask + 1, arena_cap, &st->arena_top);
                     if (off == ~0ull) { atomicAdd(&st->overflow, 1u); break; }
                     const u64 cells = long_cells(len);

@@ -717,6 +717,108 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) 
     for (u32 b = threadIdx.x; b < a.B; b += NT) a.hist[(u64)b * a.G + ss_wg(a)] = h[b];
 }
 
+// Large B, r04: the search and the histogram as two kernels.  k_ss_hist<false> ran at one
+// 1024-thread workgroup per CU (its 128 KiB histogram beside 1024 top splitters) with 75% of its
+// wave cycles waiting on the ~5 dependent L2 reads each search made below the LDS levels.
+// k_ss_find keeps SS_TOP2 top splitters' hi words in LDS (64 KiB: two workgroups per CU, twice the
+// waves) so that only ~2 levels are left for L2; an equal hi word at an LDS level decides by the
+// splitter's (lo, index) from the global arrays (exact, rare).  k_ss_count then histograms the
+// bucket ids (4 bytes per record) with the 128 KiB LDS histogram.
+#ifndef WCG_SS_SPLIT
+#define WCG_SS_SPLIT 1
+#endif
+constexpr u32 SS_TOP2 = 8192;
+constexpr int SSF_NT = 1024;
+__device__ __forceinline__ u32 ss_ntop2(const SortArgs& a) { return a.B - 1 < SS_TOP2 ? a.B - 1 : SS_TOP2; }
+__device__ __forceinline__ u32 ss_top2_index(const SortArgs& a, u32 t, u32 ntop) {
+    return (t + 1) * (a.B - 1) / (ntop + 1);     // < 8193 * 32767 < 2^32: a 32-bit division
+}
+__global__ __launch_bounds__(SSF_NT) void k_ss_find(SortArgs a) {
+    __shared__ u64 top_hi[SS_TOP2];
+    const u32 ntop = ss_ntop2(a);
+    for (u32 t = threadIdx.x; t < ntop; t += SSF_NT) top_hi[t] = a.sph[ss_top2_index(a, t, ntop)];
+    __syncthreads();
+    const u64 n = ss_count(a);
+    const u64 stride = (u64)gridDim.x * SSF_NT;
+    for (u64 i = blockIdx.x * (u64)SSF_NT + threadIdx.x; i < n; i += stride * SS_U) {
+        u64 hi[SS_U], lo[SS_U];
+        u32 si[SS_U], l[SS_U], m[SS_U];
+#pragma unroll
+        for (int k = 0; k < SS_U; k++) {
+            const u64 j = i + (u64)k * stride;
+            const Rec r = j < n ? a.rec[j] : Rec{~0ull, ~0ull, 0, 0};
+            hi[k] = r.hi; lo[k] = r.lo;
+            // an inline key searches as (key, 0) (see k_ss_hist); long keys keep their index
+            si[k] = (r.ref & LONG_FLAG) ? (u32)j : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < SS_U; k++) {
+            u32 tl = 0, th = ntop;                    // top splitters <= x (LDS, hi words)
+            while (tl < th) {
+                const u32 mid = (tl + th) >> 1;
+                const u64 sh = top_hi[mid];
+                bool lt;
+                if (hi[k] != sh) lt = hi[k] < sh;
+                else {
+                    const u32 g = ss_top2_index(a, mid, ntop);
+                    lt = key3_lt(hi[k], lo[k], si[k], sh, a.spl[g], a.spi[g]);
+                }
+                if (!lt) tl = mid + 1; else th = mid;
+            }
+            l[k] = tl > 0 ? ss_top2_index(a, tl - 1, ntop) + 1 : 0;
+            m[k] = (tl < ntop ? ss_top2_index(a, tl, ntop) : a.B - 1) - l[k];
+        }
+        while (true) {                                // lower bounds in [l, l + m), interleaved
+            bool any = false;
+            u64 sh[SS_U];
+#pragma unroll
+            for (int k = 0; k < SS_U; k++) {
+                sh[k] = m[k] ? a.sph[l[k] + m[k] / 2] : 0;
+                any |= m[k] != 0;
+            }
+            if (!any) break;
+#pragma unroll
+            for (int k = 0; k < SS_U; k++) {
+                if (!m[k]) continue;
+                const u32 half = m[k] / 2, mid = l[k] + half;
+                const bool lt = hi[k] != sh[k] ? hi[k] < sh[k]
+                                               : key3_lt(hi[k], lo[k], si[k], sh[k], a.spl[mid], a.spi[mid]);
+                if (!lt) { l[k] = mid + 1; m[k] -= half + 1; } else m[k] = half;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < SS_U; k++) {
+            const u64 j = i + (u64)k * stride;
+            if (j < n) a.bid[j] = l[k];
+        }
+    }
+}
+
+// per logical workgroup (the scatter's record ranges): bucket counts of its records, one
+// contiguous row per workgroup (k_ss_colscan turns the rows into offsets)
+__global__ __launch_bounds__(SSL_NT) void k_ss_count(SortArgs a) {
+    __shared__ u32 h[SS_MAXB];
+    for (u32 b = threadIdx.x; b < a.B; b += SSL_NT) h[b] = 0;
+    __syncthreads();
+    u64 i0, i1;
+    ss_range(a, i0, i1);
+    constexpr int CU4 = 4;                            // bucket ids per thread in flight
+    for (u64 i = i0 + threadIdx.x; i < i1; i += (u64)SSL_NT * CU4) {
+        u32 b[CU4];
+#pragma unroll
+        for (int k = 0; k < CU4; k++) {
+            const u64 j = i + (u64)k * SSL_NT;
+            b[k] = j < i1 ? a.bid[j] : ~0u;
+        }
+#pragma unroll
+        for (int k = 0; k < CU4; k++)
+            if (b[k] != ~0u) atomicAdd(&h[b[k]], 1u);
+    }
+    __syncthreads();
+    u32* row = a.hist + (u64)ss_wg(a) * a.B;
+    for (u32 b = threadIdx.x; b < a.B; b += SSL_NT) row[b] = h[b];
+}
+
 // the sample of a small sort (S <= TS_TILE) by ranks: rank = the samples below it in the
 // (hi, lo, sample index) order, a permutation.  One wave per sample: its 64 lanes compare the
 // sample with S / 64 entries each of the sample staged in LDS, and the counts are summed across
@@ -1017,7 +1119,13 @@ struct TieArgs {
     Rec* tmp;              // >= n records
     uint4* sc_key;         // >= 2n scratch items (bytes 16-31 big-endian) ...
     u32* sc_pos;           // ... and the record position
+    u64* nkeys;            // record-log jobs (the sort's distinct-key count): a long key may appear
+                           // more than once (other map calls, the table as well as the log); the
+                           // copies are merged into the first and the count lowered
 };
+__device__ __forceinline__ bool long_same(const uint8_t* base, const Rec& x, const Rec& y) {
+    return ((x.ref >> 40) & LONG_LEN_MAX) == ((y.ref >> 40) & LONG_LEN_MAX) && key_cmp_from(base, x, y, 16) == 0;
+}
 
 __device__ __forceinline__ bool tie_lt(const TieArgs& a, u64 xh, u64 xl, u32 xp, u64 yh, u64 yl, u32 yp) {
     if (xh != yh) return xh < yh;
@@ -1103,7 +1211,16 @@ __global__ __launch_bounds__(TG_NT) void k_tie_sort(TieArgs a) {
             for (u64 j = tid; j < m; j += TG_NT) a.tmp[s + j] = a.r[Q[j]];
         }
         __syncthreads();
-        for (u64 j = tid; j < m; j += TG_NT) a.r[s + j] = a.tmp[s + j];
+        u32 merged = 0;
+        for (u64 j = tid; j < m; j += TG_NT) {
+            Rec x = a.tmp[s + j];
+            if (a.nkeys) {                    // equal keys are adjacent now: the first takes the sum
+                if (j > 0 && long_same(a.base, a.tmp[s + j - 1], x)) { x.cnt = 0; merged++; }
+                else for (u64 q = j + 1; q < m && long_same(a.base, x, a.tmp[s + q]); q++) x.cnt += a.tmp[s + q].cnt;
+            }
+            a.r[s + j] = x;
+        }
+        if (merged) atomicAdd((unsigned long long*)a.nkeys, (unsigned long long)(0ull - merged));
         __syncthreads();
     }
 }
