@@ -131,10 +131,10 @@ struct wcg_ctx {
     u32 nbuckets = 64;                                // miss buckets P (<= MAX_MISS_BUCKETS)
     // ingest (wcg_ingest.h): two pinned staging buffers, two device buffers, a reader pool
     u64 chunk = 64ull << 20;
-    uint8_t* hb[2] = {nullptr, nullptr};
-    uint8_t* db[2] = {nullptr, nullptr};
+    uint8_t* hb[INGEST_SLOTS] = {};
+    uint8_t* db[INGEST_SLOTS] = {};
     uint8_t* dbig = nullptr; u64 dbig_cap = 0;
-    hipEvent_t ev_copied[2] = {}, ev_mapped[2] = {};
+    hipEvent_t ev_copied[INGEST_SLOTS] = {}, ev_mapped[INGEST_SLOTS] = {};
     hipStream_t copy_stream = nullptr;
     std::unique_ptr<TaskPool> readers;
     u64 ingest_bytes = 0;                     // bytes mapped by the last wcg_map / wcg_map_file
@@ -593,7 +593,7 @@ int partition_all(wcg_ctx* c, u32 R) {
 // ---------------------------------------------------------------- ingest
 int ingest_init(wcg_ctx* c) {
     if (c->hb[0]) return WCG_OK;
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < INGEST_SLOTS; i++) {
         HIPCHK(c, hipHostMalloc(&c->hb[i], c->chunk + SCAN_MAX_LINE + 64, hipHostMallocDefault));
         HIPCHK(c, hipMalloc(&c->db[i], c->chunk + SCAN_MAX_LINE + 64));
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
@@ -620,10 +620,36 @@ int ingest(wcg_ctx* c, u64 size, const std::function<void(uint8_t*, u64, u64)>& 
     u64 fo = 0, carry = 0, cut_prev = 0;
     int slot = 0;
     std::vector<SliceLines> sl(pool.size());
+    // the copies and map launches, in chunk order, from a thread of their own (Issuer): this
+    // thread goes on reading the next chunk meanwhile.  The context belongs to the issuer while
+    // chunks are queued; this thread touches it again only after drain().
+    std::string ierr;
+    Issuer issuer([&](int s, u64 cut) -> int {
+        if (hipSetDevice(c->device) != hipSuccess) { ierr = "hipSetDevice (ingest issuer)"; return WCG_EHIP; }
+        hipError_t e = hipStreamWaitEvent(c->copy_stream, c->ev_mapped[s], 0);   // device slot free
+        if (e == hipSuccess) e = hipMemcpyAsync(c->db[s], c->hb[s], cut, hipMemcpyHostToDevice, c->copy_stream);
+        if (e == hipSuccess) e = hipEventRecord(c->ev_copied[s], c->copy_stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_copied[s], 0);
+        if (e != hipSuccess) { ierr = std::string("ingest copy: ") + hipGetErrorString(e); return WCG_EHIP; }
+        const int rc = wcg_map_device(c, c->db[s], cut);
+        if (rc) return rc;
+        e = hipEventRecord(c->ev_mapped[s], c->stream);
+        if (e == hipSuccess) e = hipEventSynchronize(c->ev_copied[s]);       // the staging buffer is free
+        if (e != hipSuccess) { ierr = std::string("ingest copy: ") + hipGetErrorString(e); return WCG_EHIP; }
+        return WCG_OK;
+    });
+    auto drain = [&]() -> int {
+        const int rc = issuer.drain();
+        if (rc && !ierr.empty()) c->err = ierr;
+        return rc;
+    };
     while (true) {
-        HIPCHK(c, hipEventSynchronize(c->ev_copied[slot]));          // staging slot free
+        {
+            const int rc = issuer.wait_slot(slot);                    // staging slot free
+            if (rc) { (void)drain(); if (!ierr.empty()) c->err = ierr; return rc; }
+        }
         uint8_t* h = c->hb[slot];
-        if (carry) memmove(h, c->hb[slot ^ 1] + cut_prev, carry);
+        if (carry) memmove(h, c->hb[(slot + INGEST_SLOTS - 1) % INGEST_SLOTS] + cut_prev, carry);
         // the staging buffers hold chunk + SCAN_MAX_LINE bytes (a split-mode carry is < 64 KiB; a
         // DoMap-mode carry can be larger, then less is read)
         const u64 want = std::min<u64>(c->chunk + SCAN_MAX_LINE - carry, size - fo);
@@ -665,6 +691,7 @@ int ingest(wcg_ctx* c, u64 size, const std::function<void(uint8_t*, u64, u64)>& 
                 // a token or rune run longer than the chunk: map the whole rest in one call from
                 // a device buffer of its size (pathological input, e.g. 64 MiB of letters)
                 const u64 rest = len + (size - fo);
+                RC(drain());
                 RC(ensure(c, &c->dbig, &c->dbig_cap, rest + 64));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
                 HIPCHK(c, hipMemcpy(c->dbig, h, len, hipMemcpyHostToDevice));
@@ -682,21 +709,17 @@ int ingest(wcg_ctx* c, u64 size, const std::function<void(uint8_t*, u64, u64)>& 
             }
         }
         if (cut > 0) {
-            // the copy stream waits until the device slot's previous map is done
-            HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->ev_mapped[slot], 0));
-            HIPCHK(c, hipMemcpyAsync(c->db[slot], h, cut, hipMemcpyHostToDevice, c->copy_stream));
-            HIPCHK(c, hipEventRecord(c->ev_copied[slot], c->copy_stream));
-            HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_copied[slot], 0));
-            RC(wcg_map_device(c, c->db[slot], cut));
-            HIPCHK(c, hipEventRecord(c->ev_mapped[slot], c->stream));
+            issuer.push(slot, cut);       // copy (after the device slot's previous map), then map
             *mapped += cut;
+            static const bool sync_env = getenv("WCG_INGEST_SYNC") != nullptr;   // A/B: r03's order
+            if (sync_env) { const int rc = issuer.wait_slot(slot); if (rc) { (void)drain(); return rc; } }
         }
         if (stop) break;
         carry = len - cut;
         cut_prev = cut;
-        slot ^= 1;
+        slot = (slot + 1) % INGEST_SLOTS;
     }
-    return WCG_OK;
+    return drain();
 }
 
 }  // namespace
@@ -781,7 +804,7 @@ int wcg_close(wcg_ctx* c) {
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < INGEST_SLOTS; i++) {
         if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
         if (c->ev_mapped[i]) (void)hipEventDestroy(c->ev_mapped[i]);
         if (c->hb[i]) (void)hipHostFree(c->hb[i]);
@@ -1140,7 +1163,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         // k_long_agg leaves every partition cursor at zero for the next map call
         if (c->lpcur != old_cur) HIPCHK(c, hipMemsetAsync(c->lpcur, 0, LQ * sizeof(u32), ls));
         lp.ent = c->lent; lp.cur = c->lpcur;
-        k_long_hash<<<(unsigned)(grid * LONG_PARTS), LONG_NT, 0, ls>>>(a, lp, (u32)grid);
+        k_long_hash<<<(unsigned)std::min<u64>(grid * LONG_PARTS, (u64)c->ncu * 4), LONG_NT, 0, ls>>>(a, lp, (u32)grid);
 #ifndef WCG_LA_PERSIST
 #define WCG_LA_PERSIST 1
 #endif

@@ -23,6 +23,74 @@
 
 namespace wcg {
 
+// staging slots (pinned host + device buffer pairs): three, so that the reader threads can run a
+// chunk ahead of the copy when a read is slow (two kept the copy engine idle between copies)
+constexpr int INGEST_SLOTS = 3;
+
+// One thread that issues the chunks' copies and map launches in order (r04).  hipMemcpyAsync from
+// pinned memory returned only once the 64 MiB copy was done (rocprofv3 memory-copy trace of
+// wcg_map_file: the copy engine sat idle while the calling thread read the next chunk, 1.55 ms per
+// chunk against 1.27 ms of copy), so the issuing moved off the thread that reads.
+class Issuer {
+  public:
+    explicit Issuer(std::function<int(int, uint64_t)> issue) : issue_(std::move(issue)), th_([this] { loop(); }) {}
+    ~Issuer() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    // queue chunk (slot, bytes); the slot's staging buffer belongs to the issuer until released
+    void push(int slot, uint64_t n) {
+        std::lock_guard<std::mutex> g(m_);
+        q_.push_back({slot, n});
+        busy_[slot] = true;
+        cv_.notify_all();
+    }
+    // wait until the slot's staging buffer has been copied (and may be refilled); first error
+    int wait_slot(int slot) {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return !busy_[slot] || rc_ != 0; });
+        return rc_;
+    }
+    int drain() {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] {
+            for (bool b : busy_) if (b) return false;
+            return q_.empty();
+        });
+        return rc_;
+    }
+
+  private:
+    struct Item { int slot; uint64_t n; };
+    void loop() {
+        std::unique_lock<std::mutex> g(m_);
+        while (true) {
+            cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+            if (q_.empty()) return;
+            const Item it = q_.front();
+            q_.erase(q_.begin());
+            g.unlock();
+            const int rc = rc_ ? rc_ : issue_(it.slot, it.n);   // returns once the staging copy is done
+            g.lock();
+            if (rc && !rc_) rc_ = rc;
+            busy_[it.slot] = false;
+            cv_.notify_all();
+        }
+    }
+    std::function<int(int, uint64_t)> issue_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::vector<Item> q_;
+    bool busy_[INGEST_SLOTS] = {};
+    bool stop_ = false;
+    int rc_ = 0;
+    std::thread th_;
+};
+
 // fixed pool of worker threads running one batch of indexed tasks at a time
 class TaskPool {
   public:

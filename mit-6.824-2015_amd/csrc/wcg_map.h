@@ -435,6 +435,9 @@ __device__ __forceinline__ bool long_rest_same(const MapArgs& a, u64 p, u64 q, u
 // lane never waits on another's LDS write: a cache entry claimed in the same round may still have
 // no representative (rec 0), and such a lane simply emits its own entry.  A full partition falls
 // back to a fenced table insert.
+#ifndef WCG_LH_ABL
+#define WCG_LH_ABL 0      // diagnostics (wrong counts): 1 = no partition atomics, 2 = no input reads, 4 = no LDS cache
+#endif
 constexpr int LONG_NT = 256;
 constexpr int LONG_PARTS = 8;
 #ifndef WCG_LCACHE
@@ -447,19 +450,23 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
     __shared__ u64 chash[LCACHE];
     __shared__ u32 ccnt[LCACHE];
     __shared__ uint4 cw[LCACHE][2];           // representative's bytes 0-31
-    const u32 reg = blockIdx.x % nreg, part = blockIdx.x / nreg;
+    // a persistent grid over the (region, part) items: on low-cardinality text nearly every item
+    // is empty (C2: ~200 long tokens per GiB) and costs one read of its region's length, not a
+    // workgroup launch
+    for (u32 item = blockIdx.x; item < nreg * LONG_PARTS; item += gridDim.x) {
+    const u32 reg = item % nreg, part = item / nreg;
     const u32 nrec = a.llog_len[reg];
     const u64* recs = a.llog + (u64)reg * a.llog_cap;
     const u32 stride = LONG_PARTS * LONG_NT, first = part * LONG_NT;
     const u32 rounds = nrec > first ? (nrec - first + stride - 1) / stride : 0;   // workgroup-uniform
-    if (rounds == 0) return;          // ASCII text: nearly every workgroup (no barrier reached yet)
+    if (rounds == 0) continue;
     for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; crec[e] = 0; ccnt[e] = 0; }
     __syncthreads();
     auto emit = [&](u64 h, u64 rec, u64 c, const u32 (&w)[8]) {
         const u64 len = rec >> 40, p = rec & LLOG_OFF_MASK;
         const u64 tag = long_tag(h, len);
         const u32 q = long_part(tag);
-        const u32 pos = atomicAdd(&lp.cur[q], 1u);
+        const u32 pos = (WCG_LH_ABL & 1) ? (u32)(h & 63) : atomicAdd(&lp.cur[q], 1u);
         if (pos < lp.cap) {
             uint4* d = reinterpret_cast<uint4*>(lp.ent + (u64)q * lp.cap + pos);
             d[0] = make_uint4((u32)h, (u32)(h >> 32), (u32)rec, (u32)(rec >> 32));
@@ -482,7 +489,11 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
             if (len <= 15) { count_inline_run(a, p, len); len = 0; }
             else if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); len = 0; }
         }
-        if (len != 0) h = input_lhash(a, p, (u32)len, w);
+        if (len != 0) {
+            if (WCG_LH_ABL & 2) { w[0] = (u32)p; h = p * 0x9E3779B97F4A7C15ull; }   // diagnostics: no input read
+            else h = input_lhash(a, p, (u32)len, w);
+        }
+        if (len != 0 && (WCG_LH_ABL & 4)) { emit(h, p | len << 40, 1, w); len = 0; }  // diagnostics: no cache
         if (len != 0) {
             const u64 tag = long_tag(h, len), rec = p | len << 40;
             const u32 c0 = (u32)(tag >> 24) & (LCACHE - 1);
@@ -524,6 +535,8 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
         const uint4 x = cw[e][0], y = cw[e][1];
         const u32 w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
         emit(chash[e], rr, ccnt[e], w);
+    }
+    __syncthreads();                  // the cache is reused by the next item
     }
 }
 

@@ -191,6 +191,137 @@ __device__ __forceinline__ void reg_bitonic_unrolled(u64 (&h)[E], u64 (&l)[E], u
     __syncthreads();
 }
 
+// ---- r04: the same unrolled network on ONE 64-bit word per record and the position.  The word
+//      is the record's (hi, lo) order compressed to the bucket: hi - min hi over the bucket, which
+//      needs 64 - s bits (s = leading zeros of the bucket's hi range), followed by the top s bits
+//      of lo.  The compressed order agrees with (hi, lo) except inside runs of equal words, which
+//      the thread holding each run's first entry then insertion-sorts by the full (hi, lo) (an
+//      all-hi-equal bucket - C4's Greek and Cyrillic words share their first 8 bytes - compares lo
+//      alone).  A pair moves 3 dwords across lanes instead of 5 and compares 64 bits instead of
+//      128.  Records' words are clamped below all ones, the padding's word.  A bucket with a run
+//      longer than SB_RUN_MAX (records sharing a 16-byte prefix: long-key tie groups) is sorted
+//      again by the (hi, lo) network.
+#ifndef WCG_SORT_HIONLY
+#define WCG_SORT_HIONLY 1
+#endif
+#ifndef WCG_SORT_HIONLY_BIG
+#define WCG_SORT_HIONLY_BIG 1          // the 8-entry networks (buckets of 1025-2048) too
+#endif
+__device__ __forceinline__ bool h_dir_lt(bool dir, u64 x, u64 y) {
+    const bool lt = x < y, eq = x == y;
+    return (dir & lt) | (!dir & !lt & !eq);
+}
+template <int NT, int E, u32 K, u32 J>
+__device__ __forceinline__ void net_stage_hi(u64 (&h)[E], u32 (&q)[E], u64* kh, uint16_t* kp) {
+    const u32 t = threadIdx.x;
+    if constexpr (J < (u32)E) {
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            if (e & J) continue;
+            const int f = e | (int)J;
+            const bool asc = (((u32)(t * E + e)) & K) == 0;
+            const bool sw = h_dir_lt(asc, h[f], h[e]);
+            const u64 eh = h[e]; const u32 eq = q[e];
+            h[e] = sw ? h[f] : eh; q[e] = sw ? q[f] : eq;
+            h[f] = sw ? eh : h[f]; q[f] = sw ? eq : q[f];
+        }
+    } else {
+        const u32 i0 = t * E;
+        const bool keep_min = ((i0 & J) == 0) == ((i0 & K) == 0);
+        if constexpr (J < 64u * E) {
+            constexpr int D = (int)(J / E);
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const u64 ph = lane_xor64<D>(h[e]);
+                const u32 pq = lane_xor<D>(q[e]);
+                const bool take = h_dir_lt(keep_min, ph, h[e]);
+                h[e] = take ? ph : h[e]; q[e] = take ? pq : q[e];
+            }
+        } else {
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = h[e]; kp[i] = (uint16_t)q[e]; }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                const u32 i = (t * E + e) ^ J;
+                const u64 ph = kh[i]; const u32 pq = kp[i];
+                const bool take = h_dir_lt(keep_min, ph, h[e]);
+                h[e] = take ? ph : h[e]; q[e] = take ? pq : q[e];
+            }
+        }
+    }
+}
+template <int NT, int E, u32 K, u32 J>
+__device__ __forceinline__ void net_stages_j_hi(u64 (&h)[E], u32 (&q)[E], u64* kh, uint16_t* kp) {
+    net_stage_hi<NT, E, K, J>(h, q, kh, kp);
+#if WCG_SORT_NET_FENCE
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    if constexpr (J > 1) net_stages_j_hi<NT, E, K, J / 2>(h, q, kh, kp);
+}
+template <int NT, int E, u32 K>
+__device__ __forceinline__ void net_stages_k_hi(u64 (&h)[E], u32 (&q)[E], u64* kh, uint16_t* kp) {
+    net_stages_j_hi<NT, E, K, K / 2>(h, q, kh, kp);
+    if constexpr (K < (u32)NT * E) net_stages_k_hi<NT, E, K * 2>(h, q, kh, kp);
+}
+#ifndef SB_RUN_MAX
+#define SB_RUN_MAX 32
+#endif
+// w, q sorted by the compressed word: leaves (hi, lo, position) in kh/kl/kp sorted by (hi, lo)
+// over [0, m) and returns true, or false (a run longer than SB_RUN_MAX; kh/kl/kp undefined)
+template <int NT, int E>
+__device__ __forceinline__ bool reg_bitonic_unrolled_hi(u64 (&w)[E], u32 (&q)[E], const Rec* X, u32 m, u64* kh,
+                                                        u64* kl, uint16_t* kp) {
+    const u32 t = threadIdx.x;
+    net_stages_k_hi<NT, E, 2>(w, q, kh, kp);
+    __syncthreads();   // the network's last LDS stage has read kh/kp
+#pragma unroll
+    for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = w[e]; kp[i] = (uint16_t)q[e]; }
+    __syncthreads();
+    // runs of equal words: the thread with a run's first entry will sort it
+    bool too_long = false;
+    u64 runs = 0;                     // byte e: the length of the run starting at entry e (0: none)
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const u32 i = t * E + e;
+        if (i + 1 >= m || kh[i + 1] != kh[i] || (i > 0 && kh[i - 1] == kh[i])) continue;
+        u32 r = i + 2;
+        while (r < m && r - i <= SB_RUN_MAX && kh[r] == kh[i]) r++;
+        too_long |= r - i > SB_RUN_MAX;
+        runs |= (u64)(r - i) << (8 * e);
+    }
+    // the records' (hi, lo) by sorted position (the bucket's region is L2-resident)
+    u64 ch[E], cl[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const bool r = q[e] < m;
+        const Rec& x = X[r ? q[e] : 0];
+        ch[e] = r ? x.hi : ~0ull; cl[e] = r ? x.lo : ~0ull;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; e++) { const u32 i = t * E + e; kh[i] = ch[e]; kl[i] = cl[e]; }
+    if (__syncthreads_or(too_long)) return false;
+    for (; runs; runs &= runs - 1) {   // insertion sorts, one run at a time (registers: occupancy)
+        const u32 e = (u32)__builtin_ctzll(runs) >> 3;
+        const u32 i = t * E + e, r = i + (u32)(runs >> (8 * e) & 0xFF);
+        runs &= ~(0xFFull << (8 * e));
+        runs |= 1ull << (8 * e);          // the loop's own step clears this bit
+        for (u32 x = i + 1; x < r; x++) {
+            const u64 vh = kh[x], vl = kl[x];
+            const uint16_t pv = kp[x];
+            u32 y = x;
+            while (y > i && (kh[y - 1] > vh || (kh[y - 1] == vh && kl[y - 1] > vl))) {
+                kh[y] = kh[y - 1]; kl[y] = kl[y - 1]; kp[y] = kp[y - 1]; y--;
+            }
+            kh[y] = vh; kl[y] = vl; kp[y] = pv;
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
 // the loop form: (hi, lo, position) order
 template <int NT, int E>
 __device__ __forceinline__ void reg_bitonic(u64 (&h)[E], u64 (&l)[E], u32 (&q)[E], u64* kh, u64* kl, uint16_t* kp) {
@@ -1000,7 +1131,7 @@ __device__ void ss_global_sort(const SortArgs& a, u64 s, u64 m, u64* kh, u64* kl
 // load records X[0:m) as (hi, lo, position), padded to SB_NT * E entries, sort them, leave the
 // sorted entries in LDS
 template <int E>
-__device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* kl, uint16_t* kp) {
+__device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* kl, uint16_t* kp, bool cmp) {
     u64 h[E], l[E];
     u32 q[E];
     bool maxkey = false;
@@ -1010,6 +1141,44 @@ __device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* 
         if (i < m) { h[e] = X[i].hi; l[e] = X[i].lo; } else { h[e] = ~0ull; l[e] = ~0ull; }
         q[e] = i;
         maxkey |= i < m && (h[e] & l[e]) == ~0ull;
+    }
+    if (WCG_SORT_HIONLY && cmp) {
+        // the bucket's hi range: wave reductions, then one LDS word pair per wave
+        u64 mn = ~0ull, mx = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++)
+            if (threadIdx.x * E + e < m) { mn = h[e] < mn ? h[e] : mn; mx = h[e] > mx ? h[e] : mx; }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u64 a = __shfl_xor(mn, d), b = __shfl_xor(mx, d);
+            mn = a < mn ? a : mn; mx = b > mx ? b : mx;
+        }
+        __shared__ u64 rng[2][SB_NT / 64];
+        if ((threadIdx.x & 63) == 0) { rng[0][threadIdx.x >> 6] = mn; rng[1][threadIdx.x >> 6] = mx; }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < SB_NT / 64; k++) {
+            mn = rng[0][k] < mn ? rng[0][k] : mn; mx = rng[1][k] > mx ? rng[1][k] : mx;
+        }
+        const u64 range = mx - mn;
+        const u32 sh = range ? (u32)__clzll((long long)range) : 64u;   // lo bits that fit
+        u64 w[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const u64 d = h[e] - mn;
+            u64 k = sh == 64 ? l[e] : (sh == 0 ? d : (d << sh) | (l[e] >> (64 - sh)));
+            k = k == ~0ull ? ~0ull - 1 : k;
+            w[e] = threadIdx.x * E + e < m ? k : ~0ull;
+        }
+        if (reg_bitonic_unrolled_hi<SB_NT, E>(w, q, X, m, kh, kl, kp)) return;
+        // a long run: the (hi, lo) network below, from the records as they lie in LDS now (a
+        // reload from X would be merged with the first loads, keeping them live throughout)
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const u32 i = threadIdx.x * E + e;
+            h[e] = kh[i]; l[e] = kl[i]; q[e] = kp[i];
+        }
+        __syncthreads();
     }
     // The unrolled network orders (hi, lo) only, so the padding (all ones) must compare above
     // every record: a record whose prefix is all ones (no key the map produces: byte 15 is 0 or a
@@ -1036,10 +1205,10 @@ __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
     if (m > SB_CAP) { ss_global_sort(a, s, m, kh, kl, kp); return; }
     const Rec* X = a.irec + s;
     static_assert(SB_CAP == 8 * SB_NT, "k_ss_bucket's register networks cover SB_CAP entries");
-    if (BIG) sb_sort_regs<8>(X, (u32)m, kh, kl, kp);
-    else if (m <= SB_NT) sb_sort_regs<1>(X, (u32)m, kh, kl, kp);
-    else if (m <= 2 * SB_NT) sb_sort_regs<2>(X, (u32)m, kh, kl, kp);
-    else sb_sort_regs<4>(X, (u32)m, kh, kl, kp);
+    if (BIG) sb_sort_regs<8>(X, (u32)m, kh, kl, kp, WCG_SORT_HIONLY_BIG);
+    else if (m <= SB_NT) sb_sort_regs<1>(X, (u32)m, kh, kl, kp, true);
+    else if (m <= 2 * SB_NT) sb_sort_regs<2>(X, (u32)m, kh, kl, kp, true);
+    else sb_sort_regs<4>(X, (u32)m, kh, kl, kp, true);
     u32 heads = 0;
     for (u32 j = threadIdx.x; j < m; j += SB_NT) {
         Rec r = X[kp[j]];

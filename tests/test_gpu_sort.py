@@ -69,6 +69,26 @@ def test_sort_small_counts(eng, n):
     ob.assert_same(gpu_wc(eng, data), ob.merged(data))
 
 
+@pytest.mark.parametrize("tail", [1, 2])
+def test_bucket_compressed_word_runs(eng, tail):
+    """The bucket networks sort one word per record: hi minus the bucket's least hi, then as many
+    top bits of lo as fit.  Keys differing in byte 4 (a wide hi range per bucket) and again only in
+    bytes 13-14 (below the kept lo bits) tie in that word: runs of 26 are insertion-sorted by the
+    full (hi, lo); runs of 676 take the (hi, lo) network again."""
+    rng = random.Random(tail)
+    al = b"abcdefghijklmnopqrstuvwxyz"
+    ks = []
+    for c1 in al:
+        for t in range(26 ** tail):
+            suf = bytes([al[t % 26]]) if tail == 1 else bytes([al[t // 26], al[t % 26]])
+            ks.append(b"abcd" + bytes([c1]) + b"efghijkl" + suf)
+    words = ks + [rng.choice(ks) for _ in range(len(ks))]
+    rng.shuffle(words)
+    data = b" ".join(words) + b"\n"
+    ob.assert_same(gpu_wc(eng, data), ob.merged(data))
+    assert eng.stats()["keys"] == len(ks)
+
+
 def test_tie_group_of_1e5_long_keys(eng):
     """1e5 distinct keys sharing one 16-byte prefix: one tie group far above the LDS group size,
     sorted by a workgroup-wide bitonic network over scratch (not one lane)."""
