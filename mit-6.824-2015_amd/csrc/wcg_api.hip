@@ -400,13 +400,18 @@ int ensure_items(wcg_ctx* c, u64 n2) {
 
 // long keys sharing a 16-byte prefix in r[0:n): ordered by their full bytes (key bytes at
 // `base`); `tmp` is a free record buffer of n records
-int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64* nd = nullptr, u64* nkeys = nullptr) {
+// marked = true: the group starts are already listed (the sample sort's bucket kernels and
+// k_tie_edge, sort_records)
+int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64* nd = nullptr, u64* nkeys = nullptr,
+             bool marked = false) {
     if (n < 2) return WCG_OK;
     RC(ensure(c, &c->groups, &c->groups_cap, n / 2 + 2));
     RC(ensure_items(c, 2 * n));
     u64* const ng = c->d_scalar + ST_TIE_GROUPS;   // device-sized jobs: k_compact zeroed it
-    if (!nd) HIPCHK(c, hipMemsetAsync(ng, 0, sizeof(u64), c->stream));
-    k_tie_mark<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(r, n, nd, c->groups, ng);
+    if (!marked) {
+        if (!nd) HIPCHK(c, hipMemsetAsync(ng, 0, sizeof(u64), c->stream));
+        k_tie_mark<<<grid_for(n, 256, c->ncu * 4), 256, 0, c->stream>>>(r, n, nd, c->groups, ng);
+    }
     TieArgs t;
     t.r = r; t.n = n; t.nd = nd; t.base = base; t.groups = c->groups; t.ngroups = ng;
     t.tmp = tmp; t.sc_key = c->ikey; t.sc_pos = c->iidx; t.nkeys = nkeys;
@@ -415,6 +420,9 @@ int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64
     return WCG_OK;
 }
 
+#ifndef WCG_TIE_FUSED
+#define WCG_TIE_FUSED 1
+#endif
 // sample sort of recA[0:nrec) into recB (wcg_sort.h), then the tie groups
 int sort_records(wcg_ctx* c) {
     // device-sized: n is the capacity (buffers), np the count the launches are planned for
@@ -485,6 +493,17 @@ int sort_records(wcg_ctx* c) {
     a.bstart = tr ? c->hist + (u64)a.B * a.G : nullptr;
     a.irec = c->irec; a.irec2 = c->irec + n;
     a.sph = a.spl = nullptr; a.spi = nullptr;
+    // long records: from the table (nlong) and, in two-pass jobs, from the record log (lemit);
+    // their tie groups are listed by the bucket kernels and k_tie_edge (r04: k_tie_mark re-read
+    // every sorted record, 0.14 ms on C4)
+    const bool ties = n >= 2 && (dev || c->h_st->nlong + c->h_st->lemit >= 2);
+    a.groups = nullptr; a.ngroups = nullptr;
+    if (ties && WCG_TIE_FUSED) {
+        RC(ensure(c, &c->groups, &c->groups_cap, n / 2 + 2));
+        a.groups = c->groups;
+        a.ngroups = c->d_scalar + ST_TIE_GROUPS;   // device-sized jobs: k_compact zeroed it
+        if (!dev) HIPCHK(c, hipMemsetAsync(a.ngroups, 0, sizeof(u64), c->stream));
+    }
     if (!small) {                                  // the splitters as arrays (hi, lo, index)
         RC(ensure(c, &c->spx, &c->spx_cap, (u64)3 * a.B));
         a.sph = c->spx; a.spl = c->spx + a.B; a.spi = reinterpret_cast<u32*>(c->spx + 2 * a.B);
@@ -507,10 +526,9 @@ int sort_records(wcg_ctx* c) {
     else k_ss_scatter<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
     k_ss_bucket<false><<<a.B, SB_NT, 0, c->stream>>>(a);
     k_ss_bucket<true><<<a.B, SB_NT, 0, c->stream>>>(a);
+    if (a.groups) k_tie_edge<<<cdiv(a.B, TE_NT), TE_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
-    // long records: from the table (nlong) and, in two-pass jobs, from the record log (lemit)
-    if (dev || c->h_st->nlong + c->h_st->lemit >= 2)
-        RC(fix_ties(c, c->recB, n, c->arena, c->recA, a.nd, a.dedupe ? a.nkeys : nullptr));
+    if (ties) RC(fix_ties(c, c->recB, n, c->arena, c->recA, a.nd, a.dedupe ? a.nkeys : nullptr, a.groups != nullptr));
     if (c->crec == c->recA) c->compacted = false;    // recA was scratch for the ties
     if (getenv("WCG_DEBUG"))
         fprintf(stderr, "wcg: nemit %llu global_ops %llu long fallbacks %u long claims %llu\n",

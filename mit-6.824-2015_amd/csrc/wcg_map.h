@@ -444,6 +444,10 @@ constexpr int LONG_PARTS = 8;
 #define WCG_LCACHE 512
 #endif
 constexpr int LCACHE = WCG_LCACHE;            // LDS cache entries (60 B each: 512 -> 5 workgroups per CU)
+#ifndef WCG_LH_U
+#define WCG_LH_U 2
+#endif
+constexpr int LH_U = WCG_LH_U;
 __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u32 nreg) {
     __shared__ u64 ctag[LCACHE];
     __shared__ u64 crec[LCACHE];              // representative occurrence (0 = not yet set)
@@ -462,71 +466,103 @@ __global__ __launch_bounds__(LONG_NT) void k_long_hash(MapArgs a, LongPart lp, u
     if (rounds == 0) continue;
     for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) { ctag[e] = 0; crec[e] = 0; ccnt[e] = 0; }
     __syncthreads();
-    auto emit = [&](u64 h, u64 rec, u64 c, const u32 (&w)[8]) {
-        const u64 len = rec >> 40, p = rec & LLOG_OFF_MASK;
-        const u64 tag = long_tag(h, len);
-        const u32 q = long_part(tag);
-        const u32 pos = (WCG_LH_ABL & 1) ? (u32)(h & 63) : atomicAdd(&lp.cur[q], 1u);
+    // an entry into its partition at a reserved position (pos >= cap: partition full, counted here
+    // instead: fenced, exact)
+    auto put = [&](u32 q, u32 pos, u64 h, u64 rec, u64 c, const u32 (&w)[8]) {
         if (pos < lp.cap) {
             uint4* d = reinterpret_cast<uint4*>(lp.ent + (u64)q * lp.cap + pos);
             d[0] = make_uint4((u32)h, (u32)(h >> 32), (u32)rec, (u32)(rec >> 32));
             d[1] = make_uint4((u32)c, (u32)(c >> 32), 0u, 0u);
             d[2] = make_uint4(w[0], w[1], w[2], w[3]);
             d[3] = make_uint4(w[4], w[5], w[6], w[7]);
-        } else {                      // partition full: count it here (fenced, exact)
+        } else {
+            const u64 len = rec >> 40, p = rec & LLOG_OFF_MASK;
             atomicAdd(&a.st->long_fb, 1u);
-            ltab_add(a, len, tag, long_words(a, p, len, w), c, true);
+            ltab_add(a, len, long_tag(h, len), long_words(a, p, len, w), c, true);
         }
     };
-    for (u32 k = 0; k < rounds; k++) {
-        const u32 i = first + k * stride + threadIdx.x;
-        const u64 r = i < nrec ? recs[i] : 0;
-        const u64 p = r & LLOG_OFF_MASK;
-        u64 len = r >> 40, h = 0;
-        u32 w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (i < nrec && len == 0) {
-            len = long_walk(a, p);
-            if (len <= 15) { count_inline_run(a, p, len); len = 0; }
-            else if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); len = 0; }
-        }
-        if (len != 0) {
-            if (WCG_LH_ABL & 2) { w[0] = (u32)p; h = p * 0x9E3779B97F4A7C15ull; }   // diagnostics: no input read
-            else h = input_lhash(a, p, (u32)len, w);
-        }
-        if (len != 0 && (WCG_LH_ABL & 4)) { emit(h, p | len << 40, 1, w); len = 0; }  // diagnostics: no cache
-        if (len != 0) {
-            const u64 tag = long_tag(h, len), rec = p | len << 40;
-            const u32 c0 = (u32)(tag >> 24) & (LCACHE - 1);
-            bool done = false;
-            for (u32 q = 0; q < 4 && !done; q++) {
-                const u32 cs = (c0 + q) & (LCACHE - 1);
-                u64 t = ctag[cs];
+    auto emit = [&](u64 h, u64 rec, u64 c, const u32 (&w)[8]) {
+        const u32 q = long_part(long_tag(h, rec >> 40));
+        put(q, (WCG_LH_ABL & 1) ? (u32)(h & 63) : atomicAdd(&lp.cur[q], 1u), h, rec, c, w);
+    };
+    // one occurrence into the LDS cache: true when it was counted there
+    auto cache_add = [&](u64 h, u64 p, u64 len, const u32 (&w)[8]) -> bool {
+        const u64 tag = long_tag(h, len), rec = p | len << 40;
+        const u32 c0 = (u32)(tag >> 24) & (LCACHE - 1);
+        for (u32 q = 0; q < 4; q++) {
+            const u32 cs = (c0 + q) & (LCACHE - 1);
+            u64 t = ctag[cs];
+            if (t == 0) {
+                t = atomicCAS((unsigned long long*)&ctag[cs], 0ull, (unsigned long long)tag);
                 if (t == 0) {
-                    t = atomicCAS((unsigned long long*)&ctag[cs], 0ull, (unsigned long long)tag);
-                    if (t == 0) {
-                        cw[cs][0] = make_uint4(w[0], w[1], w[2], w[3]);
-                        cw[cs][1] = make_uint4(w[4], w[5], w[6], w[7]);
-                        chash[cs] = h;
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                        __hip_atomic_store(&crec[cs], rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        atomicAdd(&ccnt[cs], 1u);
-                        done = true;
-                        break;
-                    }
+                    cw[cs][0] = make_uint4(w[0], w[1], w[2], w[3]);
+                    cw[cs][1] = make_uint4(w[4], w[5], w[6], w[7]);
+                    chash[cs] = h;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __hip_atomic_store(&crec[cs], rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    atomicAdd(&ccnt[cs], 1u);
+                    return true;
                 }
-                if (t != tag) continue;
-                const u64 rr = __hip_atomic_load(&crec[cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (rr != 0 && (rr >> 40) == len) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    if (w8_same(w, cw[cs][0], cw[cs][1]) && long_rest_same(a, p, rr & LLOG_OFF_MASK, (u32)len)) {
-                        atomicAdd(&ccnt[cs], 1u);
-                        done = true;
-                    }
-                }
-                break;                // same tag, other key or not yet set: emit
             }
-            if (!done) emit(h, rec, 1, w);
+            if (t != tag) continue;
+            const u64 rr = __hip_atomic_load(&crec[cs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (rr != 0 && (rr >> 40) == len) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                if (w8_same(w, cw[cs][0], cw[cs][1]) && long_rest_same(a, p, rr & LLOG_OFF_MASK, (u32)len)) {
+                    atomicAdd(&ccnt[cs], 1u);
+                    return true;
+                }
+            }
+            return false;             // same tag, other key or not yet set: emit
         }
+        return false;
+    };
+    // LH_U records per thread and round: their input reads, and then their partition atomics,
+    // are in flight together (the round was one dependent chain: record, input words, cache,
+    // partition atomic, stores)
+    for (u32 k = 0; k < rounds; k += LH_U) {
+        u64 hh[LH_U], pp[LH_U], ll[LH_U];
+        u32 ww[LH_U][8];
+#pragma unroll
+        for (int u = 0; u < LH_U; u++) {
+            const u32 i = first + (k + u) * stride + threadIdx.x;
+            const bool live = k + u < rounds && i < nrec;
+            const u64 r = live ? recs[i] : 0;
+            pp[u] = r & LLOG_OFF_MASK;
+            ll[u] = r >> 40;
+            hh[u] = 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) ww[u][j] = 0;
+            if (live && ll[u] == 0) {             // a run to measure (length 0 in the log)
+                u64 len = long_walk(a, pp[u]);
+                if (len <= 15) { count_inline_run(a, pp[u], len); len = 0; }
+                else if (len > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); len = 0; }
+                ll[u] = len;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < LH_U; u++) {
+            if (ll[u] == 0) continue;
+            if (WCG_LH_ABL & 2) { ww[u][0] = (u32)pp[u]; hh[u] = pp[u] * 0x9E3779B97F4A7C15ull; }   // diagnostics
+            else hh[u] = input_lhash(a, pp[u], (u32)ll[u], ww[u]);
+        }
+        bool em[LH_U];
+#pragma unroll
+        for (int u = 0; u < LH_U; u++) {
+            em[u] = ll[u] != 0;
+            if (em[u] && !(WCG_LH_ABL & 4)) em[u] = !cache_add(hh[u], pp[u], ll[u], ww[u]);
+            if (LH_U > 1 && u + 1 < LH_U) __syncthreads();   // representatives of u visible to u + 1
+        }
+        u32 qq[LH_U], pos[LH_U];
+#pragma unroll
+        for (int u = 0; u < LH_U; u++) {
+            qq[u] = long_part(long_tag(hh[u], ll[u]));
+            pos[u] = 0;
+            if (em[u]) pos[u] = (WCG_LH_ABL & 1) ? (u32)(hh[u] & 63) : atomicAdd(&lp.cur[qq[u]], 1u);
+        }
+#pragma unroll
+        for (int u = 0; u < LH_U; u++)
+            if (em[u]) put(qq[u], pos[u], hh[u], pp[u] | ll[u] << 40, 1, ww[u]);
         __syncthreads();              // this round's representatives are visible to the next
     }
     for (int e = threadIdx.x; e < LCACHE; e += LONG_NT) {
@@ -774,13 +810,109 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 x) {
 //   5 = input loads only, 4 = + LDS staging and letter masks, 1 = + token starts and compaction,
 //   2 = + key extraction and hash, 3 = + LDS lookup with misses dropped; 6 = full but long
 //   tokens only counted, 7 = full but long tokens only measured and hashed
+// ---- r04: the letter mask of a wave's window with non-ASCII bytes, by a wave-wide list of the
+//      UTF-8 leads.  The lead-compacted form (utf8_mask_lds) decodes eight lead slots per lane,
+//      so a wave pays max-over-lanes (8 on C4: ~615 VALU per step, half of k_map's time there);
+//      here every lane lists its leads (window offsets, in the start list's LDS, which is built
+//      later), then the wave decodes the list 64 leads per iteration (C4: ~250 leads per step)
+//      from the staged window bytes, and each letter's span is OR-ed into its owner's mask word
+//      in LDS (bits past the chunk into the next lane's word: the carry the DPP step makes).
+//      The same decode as utf8_mask_lds (Go's utf8.DecodeRune: continuation bytes, overlongs,
+//      surrogates, > U+10FFFF), continuation bytes tested in the decoded word itself.
+#ifndef WCG_UTF8_LIST
+#define WCG_UTF8_LIST 1
+#endif
+#ifndef WCG_UL_K
+#define WCG_UL_K 1
+#endif
+constexpr int UL_K = WCG_UL_K;                // leads per lane per decode round (C4 k_map: 1 2.01-2.03 ms,
+                                              // 2 2.11, 4 2.29-2.31: the rounds past the list's end
+                                              // decode nothing at full VALU cost; 8 slots 2.04-2.06)
+__device__ __forceinline__ u32 utf8_mask_list(uint4 c, u32 nx, LdsLetters lt, const uint8_t* bytes, uint16_t* list,
+                                              uint16_t* wm, u32 lane) {
+    u32 m = (ascii_mask4(c.x & 0x7F7F7F7Fu) & ~high_mask4(c.x)) |
+            ((ascii_mask4(c.y & 0x7F7F7F7Fu) & ~high_mask4(c.y)) << 4) |
+            ((ascii_mask4(c.z & 0x7F7F7F7Fu) & ~high_mask4(c.z)) << 8) |
+            ((ascii_mask4(c.w & 0x7F7F7F7Fu) & ~high_mask4(c.w)) << 12);
+    const u32 cont = cont_mask4(c.x) | (cont_mask4(c.y) << 4) | (cont_mask4(c.z) << 8) |
+                     (cont_mask4(c.w) << 12) | (cont_mask4(nx) << 16);   // bit j: byte j
+    u32 L = (lead_mask4(c.x) | (lead_mask4(c.y) << 4) | (lead_mask4(c.z) << 8) | (lead_mask4(c.w) << 12)) &
+            (cont >> 1);                      // <= 8 per chunk (a lead's next byte is no lead)
+    const u32 nl = (u32)__popc(L);
+    const u32 incl = wave_incl_scan(nl);
+    const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+    u32 o = incl - nl;
+    wm[lane] = (uint16_t)m;
+    while (L) {
+        list[o++] = (uint16_t)(16 * lane + (u32)__builtin_ctz(L));
+        L &= L - 1;
+    }
+    wave_lds_sync();
+    u32* const wm32 = reinterpret_cast<u32*>(wm);
+    // UL_K leads per lane per round, each stage's LDS reads issued together (one round trip per
+    // stage, not per lead: the list entry, the bytes, the block id, the letter bits)
+    for (u32 base = 0; base < tot; base += 64 * UL_K) {
+        u32 p[UL_K], wd[UL_K], cp[UL_K], w[UL_K], t[UL_K], bits[UL_K];
+#pragma unroll
+        for (int k = 0; k < UL_K; k++) {           // past the list: position 0 (decodes as no letter)
+            const u32 e = list[(base + 64 * k + lane) & (MAP_SST - 1)];
+            p[k] = base + 64 * k + lane < tot ? e & (MAP_WIN - 1) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < UL_K; k++) {
+            const u32* q = reinterpret_cast<const u32*>(bytes + (p[k] & ~3u));
+            wd[k] = __builtin_amdgcn_alignbyte(q[1], q[0], p[k] & 3u);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < UL_K; k++) {
+            const bool act = base + 64 * k + lane < tot;
+            const u32 room = (u32)MAP_WIN - p[k];              // bytes past the window read as 0
+            const u32 x0 = wd[k] & (room >= 4 ? 0xFFFFFFFFu : (1u << (8 * room)) - 1u);
+            const u32 b0 = x0 & 0xFFu;                         // C2-F4 (a listed lead)
+            w[k] = __builtin_clz(~(x0 << 24));                 // 2-4
+            const u32 need = (0xFFFFFFFFu >> ((32 - 8 * w[k]) & 31)) & 0xFFFFFF00u;   // bytes 1..w-1
+            const bool conts = (((x0 & 0xC0C0C0C0u) ^ 0x80808080u) & need) == 0u;
+            const u32 x = ((b0 & (0x7Fu >> (w[k] & 31))) << 18) | ((x0 << 4) & 0x3F000u) | ((x0 >> 10) & 0xFC0u) |
+                          ((x0 >> 24) & 0x3Fu);
+            const u32 v = x >> ((24 - 6 * w[k]) & 31);
+            const bool ok = act & conts & ((v >> ((5 * w[k] - 4) & 31)) != 0u) & (v - 0xD800u >= 0x800u) &
+                            (v <= 0x10FFFFu);
+            cp[k] = ok ? v : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < UL_K; k++) {
+            const u32 b = cp[k] >> 8;
+            t[k] = lt.idx[b < LT_LDS_BLOCKS ? b : LT_LDS_BLOCKS];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < UL_K; k++) {
+            const u32 b = cp[k] >> 8;
+            bits[k] = lt.bits[(b < 8 ? b : t[k]) * 8 + ((cp[k] >> 5) & 7)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < UL_K; k++) {
+            if (!((bits[k] >> (cp[k] & 31)) & 1u)) continue;
+            const u32 own = p[k] >> 4;
+            const u32 span = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0, w[k] & 31) << (p[k] & 15u);
+            atomicOr(&wm32[own >> 1], (span & 0xFFFFu) << (16 * (own & 1)));
+            if ((span >> 16) && own < 63)                      // into the next chunk's word
+                atomicOr(&wm32[(own + 1) >> 1], (span >> 16) << (16 * ((own + 1) & 1)));
+        }
+    }
+    wave_lds_sync();
+    return wm[lane];
+}
+
 template <int ABL>
 __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs a) {
 #if !WCG_DIRECT
     __shared__ __align__(16) uint8_t wbytes[MAP_WAVES][MAP_WREG];
     __shared__ __align__(16) uint16_t wstart[MAP_WAVES][MAP_SST];
 #endif
-    __shared__ uint16_t wmask[MAP_WAVES][64];   // chunk letter masks of the wave's window
+    __shared__ __align__(4) uint16_t wmask[MAP_WAVES][64];   // chunk letter masks of the wave's window
     __shared__ __align__(16) u64 sk0[MAP_NS];
     __shared__ __align__(16) u64 mk0[MAP_NM];
     __shared__ __align__(16) u64 mk1[MAP_NM];
@@ -905,12 +1037,21 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
         // the next chunk's first dword by DPP (all lanes active; lane 63 gets zeros)
         const u32 nx = (u32)__builtin_amdgcn_update_dpp(0, (int)mine.x, 0x130, 0xF, 0xF, false);   // wave_shl:1
         u32 m;
+#if WCG_UTF8_LIST
+        if (__ballot(!all_ascii(mine)) == 0) {
+            m = ascii_mask16(mine);
+        } else {
+            m = utf8_mask_list(mine, nx, lt, bytes, sst, wmask[wave], lane);   // carries included
+            if (lane == 63 && !all_ascii(mine)) m |= 0xE000u;
+        }
+#else
         if (all_ascii(mine)) {
             m = ascii_mask16(mine);
         } else {
             m = utf8_mask_lds(mine, nx, lt);
             if (lane == 63) m |= 0xE000u;
         }
+#endif
         // bytes of this chunk covered by a letter rune that started in the previous chunk
         m = (m | ((u32)__builtin_amdgcn_update_dpp(0, (int)(m >> 16), 0x138, 0xF, 0xF, false) & 7u)) & 0xFFFFu;
         if (ABL == 4) { asm volatile("" ::"v"(m)); return 0; }

@@ -666,6 +666,7 @@ struct SortArgs {
                                     // searches' global reads stay within 20 B per splitter (L2)
     u32* bstart;             // large B (SS_TR): hist is workgroup-major [G][B] and bstart[b] the
                              // start of bucket b (k_ss_colscan); null: hist is [B][G]
+    u64* groups; u64* ngroups;   // r04: tie-group starts marked by the bucket sort (null: k_tie_mark)
 };
 
 // the records to sort: a.n, or the count the device holds (a plan made for another count only
@@ -1219,9 +1220,50 @@ __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
                 for (u32 q = j + 1; q < m && dd_same(kh[j], kl[j], kh[q], kl[q]); q++) r.cnt += X[kp[q]].cnt;
             }
         }
+        // r04: tie-group starts with both neighbours in this bucket (the first and last records:
+        // k_tie_edge); equal prefixes are both long keys or both inline (byte 15: a letter byte
+        // or 0), so the neighbours' prefixes in LDS decide
+        if (a.groups && j > 0 && j + 1 < m && (r.ref & LONG_FLAG) && kh[j + 1] == kh[j] && kl[j + 1] == kl[j] &&
+            !(kh[j - 1] == kh[j] && kl[j - 1] == kl[j]))
+            a.groups[atomicAdd((unsigned long long*)a.ngroups, 1ull)] = s + j;
         a.out[s + j] = r;
     }
     dd_count(a, heads);
+}
+
+// group start test at sorted position i (k_tie_mark's predicate)
+__device__ __forceinline__ bool tie_start(const Rec* r, u64 n, u64 i);
+// r04: the tie-group starts k_ss_bucket leaves out: every bucket's first and last records, and
+// all records of buckets past SB_CAP (sorted by the global path).  One thread per bucket; an
+// oversized bucket is scanned by the whole workgroup afterwards.
+constexpr int TE_NT = 256;
+__global__ __launch_bounds__(TE_NT) void k_tie_edge(SortArgs a) {
+    __shared__ u32 big[TE_NT];
+    __shared__ u32 nbig;
+    if (threadIdx.x == 0) nbig = 0;
+    __syncthreads();
+    const u64 n = ss_count(a);
+    const u32 b = blockIdx.x * TE_NT + threadIdx.x;
+    if (b < a.B) {
+        const u64 s = a.bstart ? a.bstart[b] : a.hist[(u64)b * a.G];
+        const u64 e = b + 1 < a.B ? (a.bstart ? a.bstart[b + 1] : a.hist[(u64)(b + 1) * a.G]) : n;
+        if (e > s) {
+            if (e - s > SB_CAP) big[atomicAdd(&nbig, 1u)] = b;
+            else {
+                if (tie_start(a.out, n, s)) a.groups[atomicAdd((unsigned long long*)a.ngroups, 1ull)] = s;
+                if (e - s > 1 && tie_start(a.out, n, e - 1))
+                    a.groups[atomicAdd((unsigned long long*)a.ngroups, 1ull)] = e - 1;
+            }
+        }
+    }
+    __syncthreads();
+    for (u32 k = 0; k < nbig; k++) {
+        const u32 bb = big[k];
+        const u64 s = a.bstart ? a.bstart[bb] : a.hist[(u64)bb * a.G];
+        const u64 e = bb + 1 < a.B ? (a.bstart ? a.bstart[bb + 1] : a.hist[(u64)(bb + 1) * a.G]) : n;
+        for (u64 i = s + threadIdx.x; i < e; i += TE_NT)
+            if (tie_start(a.out, n, i)) a.groups[atomicAdd((unsigned long long*)a.ngroups, 1ull)] = i;
+    }
 }
 
 // ---------------------------------------------------------------- tie groups
@@ -1258,17 +1300,20 @@ __device__ __forceinline__ bool same_prefix(const Rec& x, const Rec& y) { return
 
 // group starts: long keys whose successor shares their 16-byte prefix and whose predecessor
 // does not
+__device__ __forceinline__ bool tie_start(const Rec* r, u64 n, u64 i) {
+    if (i + 1 >= n) return false;
+    const Rec x = r[i], y = r[i + 1];
+    if (!rec_long(x) || !rec_long(y) || !same_prefix(x, y)) return false;
+    if (i > 0) {
+        const Rec w = r[i - 1];
+        if (rec_long(w) && same_prefix(w, x)) return false;
+    }
+    return true;
+}
 __global__ void k_tie_mark(const Rec* r, u64 n, const u64* nd, u64* groups, u64* ngroups) {
     if (nd && *nd < n) n = *nd;                  // device-sized: the sorted records only
-    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i + 1 < n; i += (u64)gridDim.x * blockDim.x) {
-        const Rec x = r[i], y = r[i + 1];
-        if (!rec_long(x) || !rec_long(y) || !same_prefix(x, y)) continue;
-        if (i > 0) {
-            const Rec w = r[i - 1];
-            if (rec_long(w) && same_prefix(w, x)) continue;
-        }
-        groups[atomicAdd(ngroups, 1ull)] = i;
-    }
+    for (u64 i = blockIdx.x * (u64)blockDim.x + threadIdx.x; i + 1 < n; i += (u64)gridDim.x * blockDim.x)
+        if (tie_start(r, n, i)) groups[atomicAdd(ngroups, 1ull)] = i;
 }
 
 // One workgroup per group (grid-stride over the group list): the group's extent, then a

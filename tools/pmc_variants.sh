@@ -1,6 +1,6 @@
 #!/bin/bash
 # Two SQ counter passes on k_map for each library given (""=default build), then a bench line per
-# library.  Usage: tools/pmc_variants.sh OUTDIR lib...
+# library.  Usage: [BENCH_ARGS='--workload ...'] tools/pmc_variants.sh OUTDIR lib...
 export TMPDIR=/tmp
 OUT=$1; shift
 mkdir -p "$OUT"
@@ -11,8 +11,8 @@ for L in "$@"; do
   i=0
   for P in "$P1" "$P2"; do
     i=$((i+1))
-    WCG_LIB=$L timeout -s KILL 60 rocprofv3 --pmc $P --kernel-include-regex k_map --output-format csv -d "$OUT/$tag/p$i" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-end-to-end > "$OUT/$tag.p$i.log" 2>&1 || exit $?
+    WCG_LIB=$L timeout -s KILL 60 rocprofv3 --pmc $P --kernel-include-regex k_map --output-format csv -d "$OUT/$tag/p$i" -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-end-to-end $BENCH_ARGS > "$OUT/$tag.p$i.log" 2>&1 || exit $?
   done
-  WCG_LIB=$L timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-end-to-end > "$OUT/$tag.bench.json" 2> "$OUT/$tag.bench.err" || exit $?
+  WCG_LIB=$L timeout -k 10 120 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-end-to-end $BENCH_ARGS > "$OUT/$tag.bench.json" 2> "$OUT/$tag.bench.err" || exit $?
   python3 tools/pmc_summary.py "$OUT/$tag" > "$OUT/$tag.pmc.txt"
 done
