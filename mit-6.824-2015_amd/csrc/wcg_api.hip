@@ -400,12 +400,15 @@ int ensure_items(wcg_ctx* c, u64 n2) {
 
 // long keys sharing a 16-byte prefix in r[0:n): ordered by their full bytes (key bytes at
 // `base`); `tmp` is a free record buffer of n records
+// tie-group lists: starts (<= n / 2), groups past TT_MAX records (<= n / (TT_MAX + 1)), past 64
+static u64 tie_list_cap(u64 n) { return (n / 2 + 2) + (n / (TT_MAX + 1) + 2) + (n / 64 + 2); }
+
 // marked = true: the group starts are already listed (the sample sort's bucket kernels and
 // k_tie_edge, sort_records)
 int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64* nd = nullptr, u64* nkeys = nullptr,
              bool marked = false) {
     if (n < 2) return WCG_OK;
-    RC(ensure(c, &c->groups, &c->groups_cap, n / 2 + 2));
+    RC(ensure(c, &c->groups, &c->groups_cap, tie_list_cap(n)));   // starts, mid and big groups
     RC(ensure_items(c, 2 * n));
     u64* const ng = c->d_scalar + ST_TIE_GROUPS;   // device-sized jobs: k_compact zeroed it
     if (!marked) {
@@ -415,6 +418,17 @@ int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64
     TieArgs t;
     t.r = r; t.n = n; t.nd = nd; t.base = base; t.groups = c->groups; t.ngroups = ng;
     t.tmp = tmp; t.sc_key = c->ikey; t.sc_pos = c->iidx; t.nkeys = nkeys;
+    // groups of <= TT_MAX records one thread each, <= 64 one wave each, the larger ones by
+    // workgroups (each kernel lists the groups it passes on after the starts)
+    u64* const mid = c->groups + (n / 2 + 2);
+    u64* const big = mid + (n / (TT_MAX + 1) + 2);
+    u64* const nmid = c->d_scalar + ST_TIE_MID;
+    u64* const nbig = c->d_scalar + ST_TIE_BIG;
+    HIPCHK(c, hipMemsetAsync(nbig, 0, 2 * sizeof(u64), c->stream));   // ST_TIE_BIG, ST_TIE_MID
+    k_tie_tiny<<<(unsigned)c->ncu * 8, 256, 0, c->stream>>>(t, mid, nmid);
+    t.groups = mid; t.ngroups = nmid;
+    k_tie_small<<<(unsigned)c->ncu * 2, TG_NT, 0, c->stream>>>(t, big, nbig);
+    t.groups = big; t.ngroups = nbig;
     k_tie_sort<<<(unsigned)c->ncu, TG_NT, 0, c->stream>>>(t);
     HIPCHK(c, hipGetLastError());
     return WCG_OK;
@@ -499,7 +513,7 @@ int sort_records(wcg_ctx* c) {
     const bool ties = n >= 2 && (dev || c->h_st->nlong + c->h_st->lemit >= 2);
     a.groups = nullptr; a.ngroups = nullptr;
     if (ties && WCG_TIE_FUSED) {
-        RC(ensure(c, &c->groups, &c->groups_cap, n / 2 + 2));
+        RC(ensure(c, &c->groups, &c->groups_cap, tie_list_cap(n)));
         a.groups = c->groups;
         a.ngroups = c->d_scalar + ST_TIE_GROUPS;   // device-sized jobs: k_compact zeroed it
         if (!dev) HIPCHK(c, hipMemsetAsync(a.ngroups, 0, sizeof(u64), c->stream));
@@ -524,8 +538,9 @@ int sort_records(wcg_ctx* c) {
     }
     if (small) k_ss_scatter<true><<<a.G, SS_NT, 0, c->stream>>>(a);
     else k_ss_scatter<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
-    k_ss_bucket<false><<<a.B, SB_NT, 0, c->stream>>>(a);
-    k_ss_bucket<true><<<a.B, SB_NT, 0, c->stream>>>(a);
+    k_ss_bucket<0><<<a.B, SB_NT, 0, c->stream>>>(a);
+    k_ss_bucket<1><<<a.B, SB_NT, 0, c->stream>>>(a);
+    k_ss_bucket<2><<<a.B, SB_NT2, 0, c->stream>>>(a);
     if (a.groups) k_tie_edge<<<cdiv(a.B, TE_NT), TE_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
     if (ties) RC(fix_ties(c, c->recB, n, c->arena, c->recA, a.nd, a.dedupe ? a.nkeys : nullptr, a.groups != nullptr));

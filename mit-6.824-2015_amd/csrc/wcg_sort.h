@@ -1045,15 +1045,16 @@ __device__ __forceinline__ bool dd_same(u64 ah, u64 al, u64 bh, u64 bl) {
     return ah == bh && al == bl && (al & 0xFFu) == 0;
 }
 // distinct keys: one atomic per workgroup
+template <int NT = SB_NT>
 __device__ __forceinline__ void dd_count(const SortArgs& a, u32 heads) {
     if (!a.dedupe) return;
-    __shared__ u32 wh[SB_NT / 64];
+    __shared__ u32 wh[NT / 64];
     for (int d = 32; d >= 1; d >>= 1) heads += __shfl_xor(heads, d, 64);
     if ((threadIdx.x & 63) == 0) wh[threadIdx.x >> 6] = heads;
     __syncthreads();
     if (threadIdx.x == 0) {
         u32 t = 0;
-        for (int w = 0; w < SB_NT / 64; w++) t += wh[w];
+        for (int w = 0; w < NT / 64; w++) t += wh[w];
         if (t) atomicAdd((unsigned long long*)a.nkeys, (unsigned long long)t);
     }
 }
@@ -1067,7 +1068,7 @@ __device__ __forceinline__ void sb_load(const Rec* X, u32 cm, u32 P, u64* kh, u6
     }
 }
 
-// Oversized bucket (more than SB_CAP records: rare with SS_OVS samples per bucket, or forced by
+// Oversized bucket (more than SB_CAP2 records: rare with SS_OVS samples per bucket, or forced by
 // WCG_SORT_TARGET in the tests): LDS-sorted chunks of SB_CAP, then pairwise merge passes between
 // irec and irec2 (thread t writes outputs [t * L / SB_NT, (t + 1) * L / SB_NT) of each pair,
 // split by merge path; A first on equal prefixes).  Equal prefixes (long keys) end up in any
@@ -1131,7 +1132,7 @@ __device__ void ss_global_sort(const SortArgs& a, u64 s, u64 m, u64* kh, u64* kl
 
 // load records X[0:m) as (hi, lo, position), padded to SB_NT * E entries, sort them, leave the
 // sorted entries in LDS
-template <int E>
+template <int NT, int E>
 __device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* kl, uint16_t* kp, bool cmp) {
     u64 h[E], l[E];
     u32 q[E];
@@ -1154,11 +1155,11 @@ __device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* 
             const u64 a = __shfl_xor(mn, d), b = __shfl_xor(mx, d);
             mn = a < mn ? a : mn; mx = b > mx ? b : mx;
         }
-        __shared__ u64 rng[2][SB_NT / 64];
+        __shared__ u64 rng[2][NT / 64];
         if ((threadIdx.x & 63) == 0) { rng[0][threadIdx.x >> 6] = mn; rng[1][threadIdx.x >> 6] = mx; }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < SB_NT / 64; k++) {
+        for (int k = 0; k < NT / 64; k++) {
             mn = rng[0][k] < mn ? rng[0][k] : mn; mx = rng[1][k] > mx ? rng[1][k] : mx;
         }
         const u64 range = mx - mn;
@@ -1171,7 +1172,7 @@ __device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* 
             k = k == ~0ull ? ~0ull - 1 : k;
             w[e] = threadIdx.x * E + e < m ? k : ~0ull;
         }
-        if (reg_bitonic_unrolled_hi<SB_NT, E>(w, q, X, m, kh, kl, kp)) return;
+        if (reg_bitonic_unrolled_hi<NT, E>(w, q, X, m, kh, kl, kp)) return;
         // a long run: the (hi, lo) network below, from the records as they lie in LDS now (a
         // reload from X would be merged with the first loads, keeping them live throughout)
 #pragma unroll
@@ -1185,33 +1186,41 @@ __device__ __forceinline__ void sb_sort_regs(const Rec* X, u32 m, u64* kh, u64* 
     // every record: a record whose prefix is all ones (no key the map produces: byte 15 is 0 or a
     // letter byte - only a crafted import or run) takes the (hi, lo, position) network.
     if (WCG_SORT_NET && (E < 8 || WCG_SORT_NET_BIG) && !__syncthreads_or(maxkey))
-        reg_bitonic_unrolled<SB_NT, E>(h, l, q, kh, kl, kp);
-    else reg_bitonic<SB_NT, E>(h, l, q, kh, kl, kp);
+        reg_bitonic_unrolled<NT, E>(h, l, q, kh, kl, kp);
+    else reg_bitonic<NT, E>(h, l, q, kh, kl, kp);
 }
 
 // one workgroup per bucket: bitonic sort of (hi, lo, position) in registers (LDS for the widest
-// stages), then the records are permuted from the bucket's region (L2-resident) into place
-// BIG = false: buckets of <= 4 * SB_NT records; true: the larger ones (their 8-entry networks
-// need more registers, which would cut the occupancy of every bucket if one kernel did both)
-template <bool BIG>
-__global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
-    constexpr u32 CAP = BIG ? SB_CAP : 4 * SB_NT;  // 18 KiB of LDS for the small kernel: 6
+// stages), then the records are permuted from the bucket's region (L2-resident) into place.
+// Size classes (their register networks need different registers and LDS, and one kernel would
+// give every bucket the largest one's occupancy): CLS 0 buckets of <= 4 * SB_NT records; CLS 1
+// up to SB_CAP (8-entry networks) and the oversized ones (> SB_CAP2: the global path); CLS 2
+// (r04) up to SB_CAP2 with 512 threads (8-entry networks: C4 at 64 GiB sorts 5e7 records in
+// 32768 buckets of ~1500, ~9% of them past SB_CAP, which the global path took)
+constexpr u32 SB_CAP2 = 4096;
+constexpr int SB_NT2 = 512;
+template <int CLS>
+__global__ __launch_bounds__(CLS == 2 ? SB_NT2 : SB_NT) void k_ss_bucket(SortArgs a) {
+    constexpr int NT = CLS == 2 ? SB_NT2 : SB_NT;
+    constexpr u32 CAP = CLS == 2 ? SB_CAP2 : CLS == 1 ? SB_CAP : 4 * SB_NT;   // 18 KiB for CLS 0: 6
     __shared__ u64 kh[CAP], kl[CAP];               // workgroups per CU (the register limit)
     __shared__ uint16_t kp[CAP];
     const u32 b = blockIdx.x;
     const u64 s = a.bstart ? a.bstart[b] : a.hist[(u64)b * a.G];
     const u64 e = b + 1 < a.B ? (a.bstart ? a.bstart[b + 1] : a.hist[(u64)(b + 1) * a.G]) : ss_count(a);
     const u64 m = e - s;
-    if (m == 0 || (m > 4 * SB_NT) != BIG) return;
-    if (m > SB_CAP) { ss_global_sort(a, s, m, kh, kl, kp); return; }
+    const int cls = m <= 4 * SB_NT ? 0 : (m <= SB_CAP || m > SB_CAP2) ? 1 : 2;
+    if (m == 0 || cls != CLS) return;
+    if (CLS == 1 && m > SB_CAP2) { ss_global_sort(a, s, m, kh, kl, kp); return; }
     const Rec* X = a.irec + s;
-    static_assert(SB_CAP == 8 * SB_NT, "k_ss_bucket's register networks cover SB_CAP entries");
-    if (BIG) sb_sort_regs<8>(X, (u32)m, kh, kl, kp, WCG_SORT_HIONLY_BIG);
-    else if (m <= SB_NT) sb_sort_regs<1>(X, (u32)m, kh, kl, kp, true);
-    else if (m <= 2 * SB_NT) sb_sort_regs<2>(X, (u32)m, kh, kl, kp, true);
-    else sb_sort_regs<4>(X, (u32)m, kh, kl, kp, true);
+    static_assert(SB_CAP == 8 * SB_NT && SB_CAP2 == 8 * SB_NT2, "k_ss_bucket's register networks cover the caps");
+    if (CLS == 2) sb_sort_regs<NT, 8>(X, (u32)m, kh, kl, kp, WCG_SORT_HIONLY_BIG);
+    else if (CLS == 1) sb_sort_regs<NT, 8>(X, (u32)m, kh, kl, kp, WCG_SORT_HIONLY_BIG);
+    else if (m <= SB_NT) sb_sort_regs<NT, 1>(X, (u32)m, kh, kl, kp, true);
+    else if (m <= 2 * SB_NT) sb_sort_regs<NT, 2>(X, (u32)m, kh, kl, kp, true);
+    else sb_sort_regs<NT, 4>(X, (u32)m, kh, kl, kp, true);
     u32 heads = 0;
-    for (u32 j = threadIdx.x; j < m; j += SB_NT) {
+    for (u32 j = threadIdx.x; j < m; j += NT) {
         Rec r = X[kp[j]];
         if (a.dedupe) {                               // sorted keys in LDS; counts from X (rare)
             if (j > 0 && dd_same(kh[j - 1], kl[j - 1], kh[j], kl[j])) r.cnt = 0;
@@ -1228,13 +1237,13 @@ __global__ __launch_bounds__(SB_NT) void k_ss_bucket(SortArgs a) {
             a.groups[atomicAdd((unsigned long long*)a.ngroups, 1ull)] = s + j;
         a.out[s + j] = r;
     }
-    dd_count(a, heads);
+    dd_count<NT>(a, heads);
 }
 
 // group start test at sorted position i (k_tie_mark's predicate)
 __device__ __forceinline__ bool tie_start(const Rec* r, u64 n, u64 i);
 // r04: the tie-group starts k_ss_bucket leaves out: every bucket's first and last records, and
-// all records of buckets past SB_CAP (sorted by the global path).  One thread per bucket; an
+// all records of buckets past SB_CAP2 (sorted by the global path).  One thread per bucket; an
 // oversized bucket is scanned by the whole workgroup afterwards.
 constexpr int TE_NT = 256;
 __global__ __launch_bounds__(TE_NT) void k_tie_edge(SortArgs a) {
@@ -1248,7 +1257,7 @@ __global__ __launch_bounds__(TE_NT) void k_tie_edge(SortArgs a) {
         const u64 s = a.bstart ? a.bstart[b] : a.hist[(u64)b * a.G];
         const u64 e = b + 1 < a.B ? (a.bstart ? a.bstart[b + 1] : a.hist[(u64)(b + 1) * a.G]) : n;
         if (e > s) {
-            if (e - s > SB_CAP) big[atomicAdd(&nbig, 1u)] = b;
+            if (e - s > SB_CAP2) big[atomicAdd(&nbig, 1u)] = b;
             else {
                 if (tie_start(a.out, n, s)) a.groups[atomicAdd((unsigned long long*)a.ngroups, 1ull)] = s;
                 if (e - s > 1 && tie_start(a.out, n, e - 1))
@@ -1286,12 +1295,24 @@ __device__ __forceinline__ u64 key_word_be(const uint8_t* base, const Rec& r, u6
 }
 
 // full bytewise order of two long keys with equal first 32 bytes (the slow path of the tie sort)
+// (r04: 16 bytes at a time when both keys sit in 16-byte aligned, zero-padded arena cells - a
+// repeated long key compares equal to its end, byte loads one dependent HBM read each)
 __device__ int key_cmp_from(const uint8_t* base, const Rec& x, const Rec& y, u64 from) {
     const u64 lx = key_bytes_len(x), ly = key_bytes_len(y);
     const uint8_t* px = base + (x.ref & LONG_OFF_MASK);
     const uint8_t* py = base + (y.ref & LONG_OFF_MASK);
     const u64 m = lx < ly ? lx : ly;
-    for (u64 i = from; i < m; i++)
+    u64 i = from;
+    if ((((uintptr_t)px | (uintptr_t)py | from) & 15) == 0) {
+        for (; i + 16 <= m; i += 16) {
+            const uint4 a = *reinterpret_cast<const uint4*>(px + i), b = *reinterpret_cast<const uint4*>(py + i);
+            const u64 a0 = bswap64((u64)a.y << 32 | a.x), b0 = bswap64((u64)b.y << 32 | b.x);
+            if (a0 != b0) return a0 < b0 ? -1 : 1;
+            const u64 a1 = bswap64((u64)a.w << 32 | a.z), b1 = bswap64((u64)b.w << 32 | b.z);
+            if (a1 != b1) return a1 < b1 ? -1 : 1;
+        }
+    }
+    for (; i < m; i++)
         if (px[i] != py[i]) return px[i] < py[i] ? -1 : 1;
     return lx < ly ? -1 : (lx > ly ? 1 : 0);
 }
@@ -1347,6 +1368,162 @@ __device__ __forceinline__ bool tie_lt(const TieArgs& a, u64 xh, u64 xl, u32 xp,
     if (xp == yp) return false;
     if (xp == ~0u || yp == ~0u) return yp == ~0u;     // padding sorts last
     return key_cmp_from(a.base, a.r[xp], a.r[yp], 32) < 0;
+}
+
+// r04: groups of <= 64 records, one wave each (16 per workgroup, no workgroup barriers).  A
+// multi-call job holds long keys that several map calls emitted (the record log, then the table
+// once the log is full): every repeated key is a tie group of 2-8 copies, ~1e6 groups on C4 at
+// 64 GiB, and a 1024-thread workgroup per group (k_tie_sort: extent, network and merge separated
+// by barriers and dependent global reads) took 120 ms there.  Larger groups are listed for
+// k_tie_sort (big / nbig).
+__device__ __forceinline__ u64 wave_shfl_up_u64(u64 v, int d) {
+    const u32 lo = (u32)__shfl_up((int)(u32)v, d, 64), hi = (u32)__shfl_up((int)(u32)(v >> 32), d, 64);
+    return (u64)hi << 32 | lo;
+}
+// tie_lt on plain values (the argument block by reference puts it in scratch)
+__device__ __forceinline__ bool tie_lt_v(const uint8_t* base, const Rec* r, u64 xh, u64 xl, u32 xp, u64 yh, u64 yl,
+                                         u32 yp) {
+    if (xh != yh) return xh < yh;
+    if (xl != yl) return xl < yl;
+    if (xp == yp) return false;
+    if (xp == ~0u || yp == ~0u) return yp == ~0u;     // padding sorts last
+    return key_cmp_from(base, r[xp], r[yp], 32) < 0;
+}
+// bytes 16-31 of a long key, big-endian (zeros past its end): one 16-byte load from an aligned,
+// zero-padded arena cell, else byte by byte (merged runs: keys inside the formatted text)
+__device__ __forceinline__ void key_words_16(const uint8_t* base, const Rec& r, u64& h, u64& l) {
+    const uint8_t* p = base + (r.ref & LONG_OFF_MASK);
+    if (((uintptr_t)p & 15) == 0) {
+        const uint4 v = *reinterpret_cast<const uint4*>(p + 16);
+        h = bswap64((u64)v.y << 32 | v.x);
+        l = bswap64((u64)v.w << 32 | v.z);
+        return;
+    }
+    h = key_word_be(base, r, 16);
+    l = key_word_be(base, r, 24);
+}
+// r04: tie groups of <= TT_MAX records, one thread each (a repeated long key of a multi-call job
+// is a group of 2-3: ~1e7 of them at 64 GiB, each a chain of dependent reads, so many must be in
+// flight at once); larger groups go to k_tie_small (mid / nmid).  A 4-entry sorting network on
+// (bytes 16-31, position); padding sorts last.
+constexpr u32 TT_MAX = 4;
+__device__ __forceinline__ void tt_cx(const uint8_t* base, const Rec* R, u64& ah, u64& al, u32& ap, u64& bh, u64& bl,
+                                      u32& bp) {
+    if (tie_lt_v(base, R, bh, bl, bp, ah, al, ap)) {
+        u64 t = ah; ah = bh; bh = t;
+        t = al; al = bl; bl = t;
+        const u32 q = ap; ap = bp; bp = q;
+    }
+}
+__global__ __launch_bounds__(256) void k_tie_tiny(TieArgs a, u64* mid, u64* nmid) {
+    const uint8_t* const base = a.base;
+    Rec* const R = a.r;
+    u64 n = a.n;
+    if (a.nd && *a.nd < n) n = *a.nd;
+    const u64 ng = *a.ngroups;
+    u64 merged = 0;
+    for (u64 g = blockIdx.x * (u64)blockDim.x + threadIdx.x; g < ng; g += (u64)gridDim.x * blockDim.x) {
+        const u64 s = a.groups[g];
+        const Rec x0 = R[s];
+        // extent, up to TT_MAX + 1 records (the reads issue together)
+        bool in[TT_MAX];
+#pragma unroll
+        for (u32 k = 1; k <= TT_MAX; k++) {
+            bool v = s + k < n;
+            if (v) { const Rec y = R[s + k]; v = rec_long(y) && same_prefix(x0, y); }
+            in[k - 1] = v;
+        }
+        u32 m = 1;
+#pragma unroll
+        for (u32 k = 0; k < TT_MAX; k++) m += (in[k] && m == k + 1) ? 1u : 0u;
+        if (m > TT_MAX) { mid[atomicAdd((unsigned long long*)nmid, 1ull)] = s; continue; }
+        u64 h0, l0, h1 = ~0ull, l1 = ~0ull, h2 = ~0ull, l2 = ~0ull, h3 = ~0ull, l3 = ~0ull;
+        u32 p0 = (u32)s, p1 = ~0u, p2 = ~0u, p3 = ~0u;
+        key_words_16(base, x0, h0, l0);
+        if (m > 1) { p1 = (u32)(s + 1); key_words_16(base, R[s + 1], h1, l1); }
+        if (m > 2) { p2 = (u32)(s + 2); key_words_16(base, R[s + 2], h2, l2); }
+        if (m > 3) { p3 = (u32)(s + 3); key_words_16(base, R[s + 3], h3, l3); }
+        tt_cx(base, R, h0, l0, p0, h1, l1, p1);
+        tt_cx(base, R, h2, l2, p2, h3, l3, p3);
+        tt_cx(base, R, h0, l0, p0, h2, l2, p2);
+        tt_cx(base, R, h1, l1, p1, h3, l3, p3);
+        tt_cx(base, R, h1, l1, p1, h2, l2, p2);
+        // the sorted records (read before any write), repeated keys merged into the first
+        Rec y0 = R[p0], y1 = m > 1 ? R[p1] : x0, y2 = m > 2 ? R[p2] : x0, y3 = m > 3 ? R[p3] : x0;
+        if (a.nkeys) {
+            if (m > 3 && long_same(base, y2, y3)) { y2.cnt += y3.cnt; y3.cnt = 0; merged++; }
+            if (m > 2 && long_same(base, y1, y2)) { y1.cnt += y2.cnt; y2.cnt = 0; merged++; }
+            if (m > 1 && long_same(base, y0, y1)) { y0.cnt += y1.cnt; y1.cnt = 0; merged++; }
+        }
+        R[s] = y0;
+        if (m > 1) R[s + 1] = y1;
+        if (m > 2) R[s + 2] = y2;
+        if (m > 3) R[s + 3] = y3;
+    }
+    for (int d = 32; d >= 1; d >>= 1) merged += __shfl_xor(merged, d, 64);
+    if ((threadIdx.x & 63) == 0 && merged) atomicAdd((unsigned long long*)a.nkeys, (unsigned long long)(0ull - merged));
+}
+
+__global__ __launch_bounds__(TG_NT) void k_tie_small(TieArgs a, u64* big, u64* nbig) {
+    const u32 lane = threadIdx.x & 63;
+    const uint8_t* const base = a.base;
+    Rec* const R = a.r;
+    u64* const nkeys = a.nkeys;
+    const u64* const groups = a.groups;
+    const u64 ng = *a.ngroups;
+    u64 n = a.n;
+    if (a.nd && *a.nd < n) n = *a.nd;
+    const u64 nw = (u64)gridDim.x * (TG_NT / 64);
+    for (u64 g = (u64)blockIdx.x * (TG_NT / 64) + (threadIdx.x >> 6); g < ng; g += nw) {
+        const u64 s = groups[g];
+        const Rec x0 = R[s];
+        // extent: the first of the next 64 records that is short or has another prefix
+        const u64 i = s + 1 + lane;
+        bool stop = i >= n;
+        if (!stop) { const Rec y = R[i]; stop = !rec_long(y) || !same_prefix(x0, y); }
+        const u64 bal = __ballot(stop);
+        if (bal == 0) {                              // > 64 records: the workgroup path
+            if (lane == 0) big[atomicAdd((unsigned long long*)nbig, 1ull)] = s;
+            continue;
+        }
+        const u32 m = 1 + (u32)__builtin_ctzll(bal);
+        const bool v = lane < m;
+        u64 th = ~0ull, tl = ~0ull;
+        u32 tp = ~0u;
+        if (v) {
+            const Rec y = R[s + lane];
+            th = key_word_be(base, y, 16); tl = key_word_be(base, y, 24); tp = (u32)(s + lane);
+        }
+        // bitonic over the first P >= m lanes (padding ~0 sorts last; lanes past P hold padding)
+        u32 P = 2;
+        while (P < m) P <<= 1;
+        for (u32 k = 2; k <= P; k <<= 1)
+            for (u32 j = k >> 1; j > 0; j >>= 1) {
+                const u64 oh = shfl_xor64(th, (int)j), ol = shfl_xor64(tl, (int)j);
+                const u32 op = (u32)__shfl_xor((int)tp, (int)j, 64);
+                const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+                const bool take = keep_min ? tie_lt_v(base, R, oh, ol, op, th, tl, tp) : tie_lt_v(base, R, th, tl, tp, oh, ol, op);
+                if (take) { th = oh; tl = ol; tp = op; }
+            }
+        Rec x = v ? R[tp] : x0;
+        if (nkeys) {                               // equal keys are adjacent: the first takes the sum
+            const u32 pp = (u32)__shfl_up((int)tp, 1, 64);
+            bool head = lane == 0 || !v;
+            if (v && lane > 0) head = !long_same(base, R[pp], x);
+            const u64 H = __ballot(head) | (~0ull << m);   // run heads (lanes past m close runs)
+            u64 c = v ? x.cnt : 0;                         // inclusive prefix sum of the counts
+            for (int d = 1; d < 64; d <<= 1) { const u64 y = wave_shfl_up_u64(c, d); if ((int)lane >= d) c += y; }
+            const u64 hi_mask = lane == 63 ? 0ull : (H >> (lane + 1));
+            const u32 end = hi_mask ? lane + 1 + (u32)__builtin_ctzll(hi_mask) : 64u;   // next head
+            const u64 last = __shfl(c, (int)(end - 1), 64);
+            const u64 before = wave_shfl_up_u64(c, 1);
+            const u64 run = last - (lane > 0 ? before : 0ull);
+            if (v) x.cnt = head ? run : 0;
+            const u32 merged = (u32)__popcll(__ballot(v && !head));
+            if (lane == 0 && merged) atomicAdd((unsigned long long*)nkeys, (unsigned long long)(0ull - merged));
+        }
+        if (v) R[s + lane] = x;
+    }
 }
 
 __global__ __launch_bounds__(TG_NT) void k_tie_sort(TieArgs a) {
