@@ -400,8 +400,8 @@ int ensure_items(wcg_ctx* c, u64 n2) {
 
 // long keys sharing a 16-byte prefix in r[0:n): ordered by their full bytes (key bytes at
 // `base`); `tmp` is a free record buffer of n records
-// tie-group lists: starts (<= n / 2), groups past TT_MAX records (<= n / (TT_MAX + 1)), past 64
-static u64 tie_list_cap(u64 n) { return (n / 2 + 2) + (n / (TT_MAX + 1) + 2) + (n / 64 + 2); }
+// tie-group lists: starts (<= n / 2), then groups past 64 records (<= n / 64)
+static u64 tie_list_cap(u64 n) { return (n / 2 + 2) + (n / 64 + 2); }
 
 // marked = true: the group starts are already listed (the sample sort's bucket kernels and
 // k_tie_edge, sort_records)
@@ -418,16 +418,12 @@ int fix_ties(wcg_ctx* c, Rec* r, u64 n, const uint8_t* base, Rec* tmp, const u64
     TieArgs t;
     t.r = r; t.n = n; t.nd = nd; t.base = base; t.groups = c->groups; t.ngroups = ng;
     t.tmp = tmp; t.sc_key = c->ikey; t.sc_pos = c->iidx; t.nkeys = nkeys;
-    // groups of <= TT_MAX records one thread each, <= 64 one wave each, the larger ones by
-    // workgroups (each kernel lists the groups it passes on after the starts)
-    u64* const mid = c->groups + (n / 2 + 2);
-    u64* const big = mid + (n / (TT_MAX + 1) + 2);
-    u64* const nmid = c->d_scalar + ST_TIE_MID;
+    // groups of <= TT_MAX records one thread each, <= 64 one wave each (one kernel), the larger
+    // ones by workgroups (listed after the starts)
+    u64* const big = c->groups + (n / 2 + 2);
     u64* const nbig = c->d_scalar + ST_TIE_BIG;
-    HIPCHK(c, hipMemsetAsync(nbig, 0, 2 * sizeof(u64), c->stream));   // ST_TIE_BIG, ST_TIE_MID
-    k_tie_tiny<<<(unsigned)c->ncu * 8, 256, 0, c->stream>>>(t, mid, nmid);
-    t.groups = mid; t.ngroups = nmid;
-    k_tie_small<<<(unsigned)c->ncu * 2, TG_NT, 0, c->stream>>>(t, big, nbig);
+    if (!marked) HIPCHK(c, hipMemsetAsync(nbig, 0, sizeof(u64), c->stream));   // else k_tie_edge zeroed it
+    k_tie_tiny<<<(unsigned)c->ncu * 8, 256, 0, c->stream>>>(t, big, nbig);
     t.groups = big; t.ngroups = nbig;
     k_tie_sort<<<(unsigned)c->ncu, TG_NT, 0, c->stream>>>(t);
     HIPCHK(c, hipGetLastError());
@@ -470,6 +466,7 @@ int sort_records(wcg_ctx* c) {
     a.nkeys = c->d_scalar + 8;                     // its own slot (the scans use d_scalar[0])
     if (a.dedupe) HIPCHK(c, hipMemsetAsync(a.nkeys, 0, sizeof(u64), c->stream));
     a.B = (u32)std::max<u64>(1, std::min<u64>(cdiv(np, target), SS_MAXB));
+    a.cls2 = np / a.B > 4 * SB_NT;                 // a 512-thread class is worth a launch
     // large sorts sample twice as densely: bucket sizes vary as 1/sqrt(samples per bucket), and a
     // bucket past 4 * SB_NT records takes the 8-entry register network (twice the work per record)
     // bucket past 4 * SB_NT records takes the 8-entry register network (twice the work per record);
@@ -511,11 +508,12 @@ int sort_records(wcg_ctx* c) {
     // their tie groups are listed by the bucket kernels and k_tie_edge (r04: k_tie_mark re-read
     // every sorted record, 0.14 ms on C4)
     const bool ties = n >= 2 && (dev || c->h_st->nlong + c->h_st->lemit >= 2);
-    a.groups = nullptr; a.ngroups = nullptr;
+    a.groups = nullptr; a.ngroups = nullptr; a.tie_zero = nullptr;
     if (ties && WCG_TIE_FUSED) {
         RC(ensure(c, &c->groups, &c->groups_cap, tie_list_cap(n)));
         a.groups = c->groups;
         a.ngroups = c->d_scalar + ST_TIE_GROUPS;   // device-sized jobs: k_compact zeroed it
+        a.tie_zero = c->d_scalar + ST_TIE_BIG;      // the big-group counter (fix_ties)
         if (!dev) HIPCHK(c, hipMemsetAsync(a.ngroups, 0, sizeof(u64), c->stream));
     }
     if (!small) {                                  // the splitters as arrays (hi, lo, index)
@@ -540,7 +538,7 @@ int sort_records(wcg_ctx* c) {
     else k_ss_scatter<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
     k_ss_bucket<0><<<a.B, SB_NT, 0, c->stream>>>(a);
     k_ss_bucket<1><<<a.B, SB_NT, 0, c->stream>>>(a);
-    k_ss_bucket<2><<<a.B, SB_NT2, 0, c->stream>>>(a);
+    if (a.cls2) k_ss_bucket<2><<<a.B, SB_NT2, 0, c->stream>>>(a);
     if (a.groups) k_tie_edge<<<cdiv(a.B, TE_NT), TE_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
     if (ties) RC(fix_ties(c, c->recB, n, c->arena, c->recA, a.nd, a.dedupe ? a.nkeys : nullptr, a.groups != nullptr));

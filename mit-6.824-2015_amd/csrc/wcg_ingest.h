@@ -13,6 +13,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -20,6 +21,8 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+
+#include "wcg_scan.h"
 
 namespace wcg {
 
@@ -146,29 +149,5 @@ class TaskPool {
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
-
-constexpr uint64_t SCAN_MAX_LINE = 65536;   // bufio.MaxScanTokenSize: a line + '\n' must fit
-
-// '\n' structure of one reader slice [a, b) of a chunk
-struct SliceLines {
-    int64_t first = -1, last = -1;   // first / last '\n' in the slice (-1: none)
-    int64_t bad = -1;                // start of the first over-long line wholly inside the slice
-};
-
-inline SliceLines scan_slice(const uint8_t* p, int64_t a, int64_t b) {
-    SliceLines s;
-    int64_t prev = -1;
-    for (int64_t i = a; i < b;) {
-        const void* q = memchr(p + i, '\n', (size_t)(b - i));
-        if (!q) break;
-        const int64_t nl = (const uint8_t*)q - p;
-        if (s.first < 0) s.first = nl;
-        else if (s.bad < 0 && nl - (prev + 1) >= (int64_t)SCAN_MAX_LINE) s.bad = prev + 1;
-        prev = nl;
-        i = nl + 1;
-    }
-    s.last = prev;
-    return s;
-}
 
 }  // namespace wcg

@@ -667,6 +667,9 @@ struct SortArgs {
     u32* bstart;             // large B (SS_TR): hist is workgroup-major [G][B] and bstart[b] the
                              // start of bucket b (k_ss_colscan); null: hist is [B][G]
     u64* groups; u64* ngroups;   // r04: tie-group starts marked by the bucket sort (null: k_tie_mark)
+    u64* tie_zero;           // r04: the tie sort's big-group counter, zeroed by k_tie_edge
+    u32 cls2;                // r04: buckets of SB_CAP..SB_CAP2 records take k_ss_bucket<2> (else the
+                             // global path: plans whose buckets average <= 1024 records)
 };
 
 // the records to sort: a.n, or the count the device holds (a plan made for another count only
@@ -1209,9 +1212,10 @@ __global__ __launch_bounds__(CLS == 2 ? SB_NT2 : SB_NT) void k_ss_bucket(SortArg
     const u64 s = a.bstart ? a.bstart[b] : a.hist[(u64)b * a.G];
     const u64 e = b + 1 < a.B ? (a.bstart ? a.bstart[b + 1] : a.hist[(u64)(b + 1) * a.G]) : ss_count(a);
     const u64 m = e - s;
-    const int cls = m <= 4 * SB_NT ? 0 : (m <= SB_CAP || m > SB_CAP2) ? 1 : 2;
+    const u64 over = a.cls2 ? SB_CAP2 : SB_CAP;     // past this: the global path (CLS 1)
+    const int cls = m <= 4 * SB_NT ? 0 : (m <= SB_CAP || m > over) ? 1 : 2;
     if (m == 0 || cls != CLS) return;
-    if (CLS == 1 && m > SB_CAP2) { ss_global_sort(a, s, m, kh, kl, kp); return; }
+    if (CLS == 1 && m > over) { ss_global_sort(a, s, m, kh, kl, kp); return; }
     const Rec* X = a.irec + s;
     static_assert(SB_CAP == 8 * SB_NT && SB_CAP2 == 8 * SB_NT2, "k_ss_bucket's register networks cover the caps");
     if (CLS == 2) sb_sort_regs<NT, 8>(X, (u32)m, kh, kl, kp, WCG_SORT_HIONLY_BIG);
@@ -1250,14 +1254,16 @@ __global__ __launch_bounds__(TE_NT) void k_tie_edge(SortArgs a) {
     __shared__ u32 big[TE_NT];
     __shared__ u32 nbig;
     if (threadIdx.x == 0) nbig = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.tie_zero) *a.tie_zero = 0;   // (a memset: 2 dispatches)
     __syncthreads();
     const u64 n = ss_count(a);
+    const u64 over = a.cls2 ? SB_CAP2 : SB_CAP;
     const u32 b = blockIdx.x * TE_NT + threadIdx.x;
     if (b < a.B) {
         const u64 s = a.bstart ? a.bstart[b] : a.hist[(u64)b * a.G];
         const u64 e = b + 1 < a.B ? (a.bstart ? a.bstart[b + 1] : a.hist[(u64)(b + 1) * a.G]) : n;
         if (e > s) {
-            if (e - s > SB_CAP2) big[atomicAdd(&nbig, 1u)] = b;
+            if (e - s > over) big[atomicAdd(&nbig, 1u)] = b;
             else {
                 if (tie_start(a.out, n, s)) a.groups[atomicAdd((unsigned long long*)a.ngroups, 1ull)] = s;
                 if (e - s > 1 && tie_start(a.out, n, e - 1))
@@ -1404,8 +1410,7 @@ __device__ __forceinline__ void key_words_16(const uint8_t* base, const Rec& r, 
 }
 // r04: tie groups of <= TT_MAX records, one thread each (a repeated long key of a multi-call job
 // is a group of 2-3: ~1e7 of them at 64 GiB, each a chain of dependent reads, so many must be in
-// flight at once); larger groups go to k_tie_small (mid / nmid).  A 4-entry sorting network on
-// (bytes 16-31, position); padding sorts last.
+// flight at once).  A 4-entry sorting network on (bytes 16-31, position); padding sorts last.
 constexpr u32 TT_MAX = 4;
 __device__ __forceinline__ void tt_cx(const uint8_t* base, const Rec* R, u64& ah, u64& al, u32& ap, u64& bh, u64& bl,
                                       u32& bp) {
@@ -1415,115 +1420,134 @@ __device__ __forceinline__ void tt_cx(const uint8_t* base, const Rec* R, u64& ah
         const u32 q = ap; ap = bp; bp = q;
     }
 }
-__global__ __launch_bounds__(256) void k_tie_tiny(TieArgs a, u64* mid, u64* nmid) {
+__device__ __forceinline__ void tie_wave_group(const uint8_t* base, Rec* R, u64 n, u64* nkeys, u64 s, u64* big,
+                                               u64* nbig, u32 lane);
+// One lane per group; groups of TT_MAX+1..64 records are then taken by the whole wave at once
+// (tie_wave_group: one kernel instead of two), larger ones listed for k_tie_sort (big / nbig).
+// The loop is wave-uniform so that every lane joins the wave's group sorts.
+__global__ __launch_bounds__(256) void k_tie_tiny(TieArgs a, u64* big, u64* nbig) {
     const uint8_t* const base = a.base;
     Rec* const R = a.r;
+    const u32 lane = threadIdx.x & 63;
     u64 n = a.n;
     if (a.nd && *a.nd < n) n = *a.nd;
     const u64 ng = *a.ngroups;
     u64 merged = 0;
-    for (u64 g = blockIdx.x * (u64)blockDim.x + threadIdx.x; g < ng; g += (u64)gridDim.x * blockDim.x) {
-        const u64 s = a.groups[g];
-        const Rec x0 = R[s];
-        // extent, up to TT_MAX + 1 records (the reads issue together)
-        bool in[TT_MAX];
+    const u64 wstride = (u64)gridDim.x * (256 / 64) * 64;
+    for (u64 g0 = ((u64)blockIdx.x * (256 / 64) + (threadIdx.x >> 6)) * 64; g0 < ng; g0 += wstride) {
+        const u64 g = g0 + lane;
+        const bool live = g < ng;
+        const u64 s = live ? a.groups[g] : 0;
+        bool is_mid = false;
+        if (live) {
+            const Rec x0 = R[s];
+            // extent, up to TT_MAX + 1 records (the reads issue together)
+            bool in[TT_MAX];
 #pragma unroll
-        for (u32 k = 1; k <= TT_MAX; k++) {
-            bool v = s + k < n;
-            if (v) { const Rec y = R[s + k]; v = rec_long(y) && same_prefix(x0, y); }
-            in[k - 1] = v;
-        }
-        u32 m = 1;
+            for (u32 k = 1; k <= TT_MAX; k++) {
+                bool v = s + k < n;
+                if (v) { const Rec y = R[s + k]; v = rec_long(y) && same_prefix(x0, y); }
+                in[k - 1] = v;
+            }
+            u32 m = 1;
 #pragma unroll
-        for (u32 k = 0; k < TT_MAX; k++) m += (in[k] && m == k + 1) ? 1u : 0u;
-        if (m > TT_MAX) { mid[atomicAdd((unsigned long long*)nmid, 1ull)] = s; continue; }
-        u64 h0, l0, h1 = ~0ull, l1 = ~0ull, h2 = ~0ull, l2 = ~0ull, h3 = ~0ull, l3 = ~0ull;
-        u32 p0 = (u32)s, p1 = ~0u, p2 = ~0u, p3 = ~0u;
-        key_words_16(base, x0, h0, l0);
-        if (m > 1) { p1 = (u32)(s + 1); key_words_16(base, R[s + 1], h1, l1); }
-        if (m > 2) { p2 = (u32)(s + 2); key_words_16(base, R[s + 2], h2, l2); }
-        if (m > 3) { p3 = (u32)(s + 3); key_words_16(base, R[s + 3], h3, l3); }
-        tt_cx(base, R, h0, l0, p0, h1, l1, p1);
-        tt_cx(base, R, h2, l2, p2, h3, l3, p3);
-        tt_cx(base, R, h0, l0, p0, h2, l2, p2);
-        tt_cx(base, R, h1, l1, p1, h3, l3, p3);
-        tt_cx(base, R, h1, l1, p1, h2, l2, p2);
-        // the sorted records (read before any write), repeated keys merged into the first
-        Rec y0 = R[p0], y1 = m > 1 ? R[p1] : x0, y2 = m > 2 ? R[p2] : x0, y3 = m > 3 ? R[p3] : x0;
-        if (a.nkeys) {
-            if (m > 3 && long_same(base, y2, y3)) { y2.cnt += y3.cnt; y3.cnt = 0; merged++; }
-            if (m > 2 && long_same(base, y1, y2)) { y1.cnt += y2.cnt; y2.cnt = 0; merged++; }
-            if (m > 1 && long_same(base, y0, y1)) { y0.cnt += y1.cnt; y1.cnt = 0; merged++; }
+            for (u32 k = 0; k < TT_MAX; k++) m += (in[k] && m == k + 1) ? 1u : 0u;
+            is_mid = m > TT_MAX;
+            if (!is_mid) {
+                u64 h0, l0, h1 = ~0ull, l1 = ~0ull, h2 = ~0ull, l2 = ~0ull, h3 = ~0ull, l3 = ~0ull;
+                u32 p0 = (u32)s, p1 = ~0u, p2 = ~0u, p3 = ~0u;
+                key_words_16(base, x0, h0, l0);
+                if (m > 1) { p1 = (u32)(s + 1); key_words_16(base, R[s + 1], h1, l1); }
+                if (m > 2) { p2 = (u32)(s + 2); key_words_16(base, R[s + 2], h2, l2); }
+                if (m > 3) { p3 = (u32)(s + 3); key_words_16(base, R[s + 3], h3, l3); }
+                tt_cx(base, R, h0, l0, p0, h1, l1, p1);
+                tt_cx(base, R, h2, l2, p2, h3, l3, p3);
+                tt_cx(base, R, h0, l0, p0, h2, l2, p2);
+                tt_cx(base, R, h1, l1, p1, h3, l3, p3);
+                tt_cx(base, R, h1, l1, p1, h2, l2, p2);
+                // the sorted records (read before any write), repeated keys merged into the first
+                Rec y0 = R[p0], y1 = m > 1 ? R[p1] : x0, y2 = m > 2 ? R[p2] : x0, y3 = m > 3 ? R[p3] : x0;
+                if (a.nkeys) {
+                    if (m > 3 && long_same(base, y2, y3)) { y2.cnt += y3.cnt; y3.cnt = 0; merged++; }
+                    if (m > 2 && long_same(base, y1, y2)) { y1.cnt += y2.cnt; y2.cnt = 0; merged++; }
+                    if (m > 1 && long_same(base, y0, y1)) { y0.cnt += y1.cnt; y1.cnt = 0; merged++; }
+                }
+                R[s] = y0;
+                if (m > 1) R[s + 1] = y1;
+                if (m > 2) R[s + 2] = y2;
+                if (m > 3) R[s + 3] = y3;
+            }
         }
-        R[s] = y0;
-        if (m > 1) R[s + 1] = y1;
-        if (m > 2) R[s + 2] = y2;
-        if (m > 3) R[s + 3] = y3;
+        for (u64 mm = __ballot(is_mid); mm; mm &= mm - 1) {   // the larger groups, the whole wave each
+            const int src = (int)__builtin_ctzll(mm);
+            const u64 sm = (u64)(u32)__shfl((int)(u32)s, src, 64) | (u64)(u32)__shfl((int)(u32)(s >> 32), src, 64) << 32;
+            tie_wave_group(base, R, n, a.nkeys, sm, big, nbig, lane);
+        }
     }
     for (int d = 32; d >= 1; d >>= 1) merged += __shfl_xor(merged, d, 64);
     if ((threadIdx.x & 63) == 0 && merged) atomicAdd((unsigned long long*)a.nkeys, (unsigned long long)(0ull - merged));
 }
 
+// one tie group of <= 64 records starting at s, by the whole wave (all 64 lanes active); a larger
+// group is listed for k_tie_sort
+__device__ __forceinline__ void tie_wave_group(const uint8_t* base, Rec* R, u64 n, u64* nkeys, u64 s, u64* big,
+                                               u64* nbig, u32 lane) {
+    const Rec x0 = R[s];
+    // extent: the first of the next 64 records that is short or has another prefix
+    const u64 i = s + 1 + lane;
+    bool stop = i >= n;
+    if (!stop) { const Rec y = R[i]; stop = !rec_long(y) || !same_prefix(x0, y); }
+    const u64 bal = __ballot(stop);
+    if (bal == 0) {                              // > 64 records: the workgroup path
+        if (lane == 0) big[atomicAdd((unsigned long long*)nbig, 1ull)] = s;
+        return;
+    }
+    const u32 m = 1 + (u32)__builtin_ctzll(bal);
+    const bool v = lane < m;
+    u64 th = ~0ull, tl = ~0ull;
+    u32 tp = ~0u;
+    if (v) {
+        const Rec y = R[s + lane];
+        th = key_word_be(base, y, 16); tl = key_word_be(base, y, 24); tp = (u32)(s + lane);
+    }
+    // bitonic over the first P >= m lanes (padding ~0 sorts last; lanes past P hold padding)
+    u32 P = 2;
+    while (P < m) P <<= 1;
+    for (u32 k = 2; k <= P; k <<= 1)
+        for (u32 j = k >> 1; j > 0; j >>= 1) {
+            const u64 oh = shfl_xor64(th, (int)j), ol = shfl_xor64(tl, (int)j);
+            const u32 op = (u32)__shfl_xor((int)tp, (int)j, 64);
+            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+            const bool take = keep_min ? tie_lt_v(base, R, oh, ol, op, th, tl, tp) : tie_lt_v(base, R, th, tl, tp, oh, ol, op);
+            if (take) { th = oh; tl = ol; tp = op; }
+        }
+    Rec x = v ? R[tp] : x0;
+    if (nkeys) {                               // equal keys are adjacent: the first takes the sum
+        const u32 pp = (u32)__shfl_up((int)tp, 1, 64);
+        bool head = lane == 0 || !v;
+        if (v && lane > 0) head = !long_same(base, R[pp], x);
+        const u64 H = __ballot(head) | (~0ull << m);   // run heads (lanes past m close runs)
+        u64 c = v ? x.cnt : 0;                         // inclusive prefix sum of the counts
+        for (int d = 1; d < 64; d <<= 1) { const u64 y = wave_shfl_up_u64(c, d); if ((int)lane >= d) c += y; }
+        const u64 hi_mask = lane == 63 ? 0ull : (H >> (lane + 1));
+        const u32 end = hi_mask ? lane + 1 + (u32)__builtin_ctzll(hi_mask) : 64u;   // next head
+        const u64 last = __shfl(c, (int)(end - 1), 64);
+        const u64 before = wave_shfl_up_u64(c, 1);
+        const u64 run = last - (lane > 0 ? before : 0ull);
+        if (v) x.cnt = head ? run : 0;
+        const u32 merged = (u32)__popcll(__ballot(v && !head));
+        if (lane == 0 && merged) atomicAdd((unsigned long long*)nkeys, (unsigned long long)(0ull - merged));
+    }
+    if (v) R[s + lane] = x;
+}
 __global__ __launch_bounds__(TG_NT) void k_tie_small(TieArgs a, u64* big, u64* nbig) {
     const u32 lane = threadIdx.x & 63;
-    const uint8_t* const base = a.base;
-    Rec* const R = a.r;
-    u64* const nkeys = a.nkeys;
-    const u64* const groups = a.groups;
-    const u64 ng = *a.ngroups;
     u64 n = a.n;
     if (a.nd && *a.nd < n) n = *a.nd;
+    const u64 ng = *a.ngroups;
     const u64 nw = (u64)gridDim.x * (TG_NT / 64);
-    for (u64 g = (u64)blockIdx.x * (TG_NT / 64) + (threadIdx.x >> 6); g < ng; g += nw) {
-        const u64 s = groups[g];
-        const Rec x0 = R[s];
-        // extent: the first of the next 64 records that is short or has another prefix
-        const u64 i = s + 1 + lane;
-        bool stop = i >= n;
-        if (!stop) { const Rec y = R[i]; stop = !rec_long(y) || !same_prefix(x0, y); }
-        const u64 bal = __ballot(stop);
-        if (bal == 0) {                              // > 64 records: the workgroup path
-            if (lane == 0) big[atomicAdd((unsigned long long*)nbig, 1ull)] = s;
-            continue;
-        }
-        const u32 m = 1 + (u32)__builtin_ctzll(bal);
-        const bool v = lane < m;
-        u64 th = ~0ull, tl = ~0ull;
-        u32 tp = ~0u;
-        if (v) {
-            const Rec y = R[s + lane];
-            th = key_word_be(base, y, 16); tl = key_word_be(base, y, 24); tp = (u32)(s + lane);
-        }
-        // bitonic over the first P >= m lanes (padding ~0 sorts last; lanes past P hold padding)
-        u32 P = 2;
-        while (P < m) P <<= 1;
-        for (u32 k = 2; k <= P; k <<= 1)
-            for (u32 j = k >> 1; j > 0; j >>= 1) {
-                const u64 oh = shfl_xor64(th, (int)j), ol = shfl_xor64(tl, (int)j);
-                const u32 op = (u32)__shfl_xor((int)tp, (int)j, 64);
-                const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-                const bool take = keep_min ? tie_lt_v(base, R, oh, ol, op, th, tl, tp) : tie_lt_v(base, R, th, tl, tp, oh, ol, op);
-                if (take) { th = oh; tl = ol; tp = op; }
-            }
-        Rec x = v ? R[tp] : x0;
-        if (nkeys) {                               // equal keys are adjacent: the first takes the sum
-            const u32 pp = (u32)__shfl_up((int)tp, 1, 64);
-            bool head = lane == 0 || !v;
-            if (v && lane > 0) head = !long_same(base, R[pp], x);
-            const u64 H = __ballot(head) | (~0ull << m);   // run heads (lanes past m close runs)
-            u64 c = v ? x.cnt : 0;                         // inclusive prefix sum of the counts
-            for (int d = 1; d < 64; d <<= 1) { const u64 y = wave_shfl_up_u64(c, d); if ((int)lane >= d) c += y; }
-            const u64 hi_mask = lane == 63 ? 0ull : (H >> (lane + 1));
-            const u32 end = hi_mask ? lane + 1 + (u32)__builtin_ctzll(hi_mask) : 64u;   // next head
-            const u64 last = __shfl(c, (int)(end - 1), 64);
-            const u64 before = wave_shfl_up_u64(c, 1);
-            const u64 run = last - (lane > 0 ? before : 0ull);
-            if (v) x.cnt = head ? run : 0;
-            const u32 merged = (u32)__popcll(__ballot(v && !head));
-            if (lane == 0 && merged) atomicAdd((unsigned long long*)nkeys, (unsigned long long)(0ull - merged));
-        }
-        if (v) R[s + lane] = x;
-    }
+    for (u64 g = (u64)blockIdx.x * (TG_NT / 64) + (threadIdx.x >> 6); g < ng; g += nw)
+        tie_wave_group(a.base, a.r, n, a.nkeys, a.groups[g], big, nbig, lane);
 }
 
 __global__ __launch_bounds__(TG_NT) void k_tie_sort(TieArgs a) {
