@@ -73,7 +73,7 @@ __device__ __forceinline__ u64 long_home(u64 s, u64 len, u64 lslots, u64 heap_ca
 // ---- device-side counters/status (one per context)
 constexpr u64 ST_SCALAR_OFF = 128;   // the scalars follow DevState in one allocation (wcg_api.hip)
 constexpr u64 ST_TIE_GROUPS = 16;    // scalar slot of the tie-group count (the scans use 0, the sort 8)
-constexpr u64 ST_TIE_BIG = 17;       // scalar slot: tie groups of more than 64 records (k_tie_small)
+constexpr u64 ST_TIE_BIG = 17;       // scalar slot: tie groups of more than 64 records (k_tie_tiny -> k_tie_sort)
 constexpr u64 ST_GLIST = 24;         // scalar slot: two-pass contexts' global-table claim list, or 0
 constexpr u64 GLIST_CAP = 1ull << 20;   // claims listed (more: compaction and reset scan it all)
 constexpr u64 ST_LLIST = 25;         // scalar slot: large contexts' long-key-table claim list, or 0

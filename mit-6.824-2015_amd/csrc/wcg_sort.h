@@ -1540,16 +1540,6 @@ __device__ __forceinline__ void tie_wave_group(const uint8_t* base, Rec* R, u64 
     }
     if (v) R[s + lane] = x;
 }
-__global__ __launch_bounds__(TG_NT) void k_tie_small(TieArgs a, u64* big, u64* nbig) {
-    const u32 lane = threadIdx.x & 63;
-    u64 n = a.n;
-    if (a.nd && *a.nd < n) n = *a.nd;
-    const u64 ng = *a.ngroups;
-    const u64 nw = (u64)gridDim.x * (TG_NT / 64);
-    for (u64 g = (u64)blockIdx.x * (TG_NT / 64) + (threadIdx.x >> 6); g < ng; g += nw)
-        tie_wave_group(a.base, a.r, n, a.nkeys, a.groups[g], big, nbig, lane);
-}
-
 __global__ __launch_bounds__(TG_NT) void k_tie_sort(TieArgs a) {
     __shared__ u64 th[TG_CAP], tl[TG_CAP];
     __shared__ u32 tp[TG_CAP];
