@@ -120,7 +120,17 @@ __device__ __forceinline__ void agg_decode(const u64 (&u)[6], u64 (&k0)[4], u64 
     }
 WCG_AGG_SET_OPS(A)
 WCG_AGG_SET_OPS(B)
+WCG_AGG_SET_OPS(C)
 #undef WCG_AGG_SET_OPS
+// register sets (batches in flight per wave).  r04 measured a third (C2's pass 1 spends 54% of
+// its wave cycles waiting with two): pass 1 0.284-0.292 ms with three against 0.288-0.293 with
+// two, pass 2 1.29-1.33 ms either way (profiles/r04_kagg_three_sets.txt): two kept
+#ifndef WCG_AGG_SETS1
+#define WCG_AGG_SETS1 2
+#endif
+#ifndef WCG_AGG_SETS2
+#define WCG_AGG_SETS2 2
+#endif
 
 // One (bucket, slice) of k_agg: index bi = p + P * s.  Returns the global-table inserts made.
 // MODE is a template parameter: one kernel for both passes held the union of their registers
@@ -276,26 +286,55 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
     // top of every batch (s_waitcnt vmcnt(0)), exposing one HBM latency per batch.  Loads are
     // unconditional (a dead batch reads the first region's first batch), so the count never
     // depends on which batches are live.  An overflow insert waits for all loads itself (harmless).
-    u32 kA = 0, bA = 0, kB, bB;
+    constexpr int NSETS = emit ? WCG_AGG_SETS2 : WCG_AGG_SETS1;
+    static_assert(NSETS == 2 || NSETS == 3, "k_agg's batch walk names two or three register sets");
+    u32 kA = 0, bA = 0, kB, bB, kC = 0, bC = 0;
     if (per_wave) { kA = wave; bA = (u32)-1; advance(kA, bA, WSTRIDE); }
     else advance(kA, bA, wave);
     kB = kA; bB = bA;
     advance(kB, bB, WSTRIDE);
-    v4u a0, a1, a2, b0, b1, b2;
+    v4u a0, a1, a2, b0, b1, b2, c0, c1, c2;
     agg_load_A(batch_ptr(kA, bA), a0, a1, a2);
     agg_load_B(batch_ptr(kB, bB), b0, b1, b2);
-    while (kA < nk) {
-        agg_wait_A<3>(a0, a1, a2);
-        process(kA, bA, a0, a1, a2);
-        kA = kB; bA = bB;
-        advance(kA, bA, WSTRIDE);
-        agg_load_A(batch_ptr(kA, bA), a0, a1, a2);
-        if (kB >= nk) break;
-        agg_wait_B<3>(b0, b1, b2);
-        process(kB, bB, b0, b1, b2);
-        kB = kA; bB = bA;
-        advance(kB, bB, WSTRIDE);
-        agg_load_B(batch_ptr(kB, bB), b0, b1, b2);
+    if (NSETS == 3) {
+        // batch g in A, g + 1 in B, g + 2 in C; each wait leaves the other two sets' six loads in flight
+        kC = kB; bC = bB;
+        advance(kC, bC, WSTRIDE);
+        agg_load_C(batch_ptr(kC, bC), c0, c1, c2);
+        while (kA < nk) {
+            agg_wait_A<6>(a0, a1, a2);
+            process(kA, bA, a0, a1, a2);
+            kA = kC; bA = bC;
+            advance(kA, bA, WSTRIDE);
+            agg_load_A(batch_ptr(kA, bA), a0, a1, a2);
+            if (kB >= nk) break;
+            agg_wait_B<6>(b0, b1, b2);
+            process(kB, bB, b0, b1, b2);
+            kB = kA; bB = bA;
+            advance(kB, bB, WSTRIDE);
+            agg_load_B(batch_ptr(kB, bB), b0, b1, b2);
+            if (kC >= nk) break;
+            agg_wait_C<6>(c0, c1, c2);
+            process(kC, bC, c0, c1, c2);
+            kC = kB; bC = bB;
+            advance(kC, bC, WSTRIDE);
+            agg_load_C(batch_ptr(kC, bC), c0, c1, c2);
+        }
+        agg_wait_C<0>(c0, c1, c2);                    // nothing may land in a dead register
+    } else {
+        while (kA < nk) {
+            agg_wait_A<3>(a0, a1, a2);
+            process(kA, bA, a0, a1, a2);
+            kA = kB; bA = bB;
+            advance(kA, bA, WSTRIDE);
+            agg_load_A(batch_ptr(kA, bA), a0, a1, a2);
+            if (kB >= nk) break;
+            agg_wait_B<3>(b0, b1, b2);
+            process(kB, bB, b0, b1, b2);
+            kB = kA; bB = bA;
+            advance(kB, bB, WSTRIDE);
+            agg_load_B(batch_ptr(kB, bB), b0, b1, b2);
+        }
     }
     agg_wait_A<0>(a0, a1, a2);                        // nothing may land in a dead register
     agg_wait_B<0>(b0, b1, b2);
