@@ -624,6 +624,8 @@ int partition_all(wcg_ctx* c, u32 R) {
 // ---------------------------------------------------------------- ingest
 int ingest_init(wcg_ctx* c) {
     if (c->hb[0]) return WCG_OK;
+    // measurement knobs: chunk bytes (default 64 MiB) and reader threads (default min(16, cores))
+    if (const char* e = getenv("WCG_INGEST_CHUNK_MIB")) c->chunk = std::max<u64>(1, strtoull(e, nullptr, 10)) << 20;
     for (int i = 0; i < INGEST_SLOTS; i++) {
         HIPCHK(c, hipHostMalloc(&c->hb[i], c->chunk + SCAN_MAX_LINE + 64, hipHostMallocDefault));
         HIPCHK(c, hipMalloc(&c->db[i], c->chunk + SCAN_MAX_LINE + 64));
@@ -632,7 +634,9 @@ int ingest_init(wcg_ctx* c) {
     }
     HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     unsigned hw = std::thread::hardware_concurrency();
-    c->readers.reset(new TaskPool((int)std::max(1u, std::min(16u, hw ? hw : 1u))));
+    unsigned nr = std::max(1u, std::min(16u, hw ? hw : 1u));
+    if (const char* e = getenv("WCG_INGEST_READERS")) nr = std::max(1u, std::min(64u, (unsigned)atoi(e)));
+    c->readers.reset(new TaskPool((int)nr));
     return WCG_OK;
 }
 
