@@ -1376,12 +1376,12 @@ __device__ __forceinline__ bool tie_lt(const TieArgs& a, u64 xh, u64 xl, u32 xp,
     return key_cmp_from(a.base, a.r[xp], a.r[yp], 32) < 0;
 }
 
-// r04: groups of <= 64 records, one wave each (16 per workgroup, no workgroup barriers).  A
-// multi-call job holds long keys that several map calls emitted (the record log, then the table
-// once the log is full): every repeated key is a tie group of 2-8 copies, ~1e6 groups on C4 at
-// 64 GiB, and a 1024-thread workgroup per group (k_tie_sort: extent, network and merge separated
-// by barriers and dependent global reads) took 120 ms there.  Larger groups are listed for
-// k_tie_sort (big / nbig).
+// r04: small tie groups without workgroup barriers.  A multi-call job holds long keys that
+// several map calls emitted (the record log, then the table once the log is full): every
+// repeated key is a tie group of 2-8 copies, and a 1024-thread workgroup per group (k_tie_sort:
+// extent, network and merge separated by barriers and dependent global reads) took 120 ms on C4
+// at 64 GiB.  Groups of <= TT_MAX records take one thread each, <= 64 one wave each
+// (tie_wave_group, in the same kernel); larger ones are listed for k_tie_sort (big / nbig).
 __device__ __forceinline__ u64 wave_shfl_up_u64(u64 v, int d) {
     const u32 lo = (u32)__shfl_up((int)(u32)v, d, 64), hi = (u32)__shfl_up((int)(u32)(v >> 32), d, 64);
     return (u64)hi << 32 | lo;
@@ -1409,7 +1409,7 @@ __device__ __forceinline__ void key_words_16(const uint8_t* base, const Rec& r, 
     l = key_word_be(base, r, 24);
 }
 // r04: tie groups of <= TT_MAX records, one thread each (a repeated long key of a multi-call job
-// is a group of 2-3: ~1e7 of them at 64 GiB, each a chain of dependent reads, so many must be in
+// is a group of 2-3, one per repeated key - each a chain of dependent reads, so many must be in
 // flight at once).  A 4-entry sorting network on (bytes 16-31, position); padding sorts last.
 constexpr u32 TT_MAX = 4;
 __device__ __forceinline__ void tt_cx(const uint8_t* base, const Rec* R, u64& ah, u64& al, u32& ap, u64& bh, u64& bl,
