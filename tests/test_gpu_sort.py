@@ -45,10 +45,11 @@ def _vocab_text(rng, nkeys, long_frac=0.1):
     return b" ".join(words) + b"\n"
 
 
-@pytest.mark.parametrize("target", [None, "64", "1000000"])
+@pytest.mark.parametrize("target", [None, "64", "3000", "1000000"])
 def test_sample_sort_bucket_paths(eng, target):
-    """Default buckets; tiny buckets (many, through the sample merge sort); one bucket larger than
-    the LDS sort (the in-workgroup global merge path)."""
+    """Default buckets; tiny buckets (many, through the sample merge sort); buckets of ~3000 (the
+    512-thread class of 2049-4096 records, r04); one bucket larger than the LDS sort (the
+    in-workgroup global merge path)."""
     data = _vocab_text(random.Random(2), 150_000)
     old = os.environ.get("WCG_SORT_TARGET")
     try:
