@@ -50,7 +50,9 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N > 1 path with host-staged records, ranks may share a GPU")
-    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+    # below the driver's 600 s bench limit, so that the launcher's own bounded stop (and every
+    # rank's stack dump on SIGTERM) happens before an outside kill
+    ap.add_argument("--launch-timeout", type=float, default=480.0,
                     help="--gpus N > 1 without an external launcher: seconds before the rank processes are stopped")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per map launch (written by tools/pmc_traffic.py)")
@@ -287,16 +289,38 @@ def main():
         # RCCL inside libwcg: wcg_exchange (the shuffle) and wcg_gather_merge (Merge at rank 0)
         wd.init_comm(teng)
 
+    # N > 1: each rank names the stage it enters on stderr for the first warm-up step and the first
+    # timed step (a hang is then attributed to map / exchange / reduce / gather), and dumps every
+    # thread's stack when the launcher stops it (SIGTERM)
+    nstep = [0]
+    mark_steps = {0, args.warmup}
+
+    def stage(name):
+        if world > 1 and nstep[0] in mark_steps:
+            sys.stderr.write(f"bench rank {rank}/{world}: step {nstep[0]} {name}\n")
+            sys.stderr.flush()
+
+    if world > 1:
+        import faulthandler
+        import signal
+        faulthandler.register(signal.SIGTERM, chain=True)
+
     def step():
         """one job: this rank's map (N = 1: + DoReduce and Merge; N > 1: + shuffle, owners'
         DoReduce, Merge of the runs at rank 0)"""
+        stage("map")
         eng.reset()
         eng.map_device(dev.data_ptr(), n)
         if world == 1:
             eng.reduce()
+            nstep[0] += 1
             return
+        stage("exchange+reduce")
         wd.shuffle_reduce(teng, args.nreduce)            # owners: DoReduce of their partitions
+        stage("gather")
         wd.gather_merge(teng, fetch=False)               # rank 0: k-way merge of the sorted runs
+        stage("done")
+        nstep[0] += 1
 
     for _ in range(args.warmup):
         step()
@@ -425,7 +449,8 @@ def main():
                        "parallelism": f"{world} ranks, one line-aligned range each",
                        "shuffle": None if world == 1 else
                        ("gloo rehearsal, host-staged" if gloo else
-                        "RCCL all_to_all_single (counts, then records); owners sort; rank 0 merges the runs")},
+                        "wcg_exchange: RCCL allgather of the count rows, grouped ncclSend/ncclRecv of the "
+                        "32-byte units; owners sort; wcg_gather_merge: runs to rank 0, k-way merge")},
             "roofline": {"bound": "hbm", "kernel": "wcg::k_map",
                          "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

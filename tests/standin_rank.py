@@ -4,6 +4,7 @@ runs at rank 0; wcg/distributed.py) over gloo with the oracle-backed stand-in en
 tests/test_distributed.py.  Rank 0 prints one JSON line, as bench.py does.
 
   python -m torch.distributed.run ... tests/standin_rank.py [--fail-rank R] [--hang-rank R]
+                                      [--ignore-term-rank R] [--pid-dir D]
 """
 import argparse
 import json
@@ -21,6 +22,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fail-rank", type=int, default=-1)
     ap.add_argument("--hang-rank", type=int, default=-1)
+    ap.add_argument("--ignore-term-rank", type=int, default=-1,
+                    help="this rank ignores SIGTERM and hangs (only SIGKILL ends it)")
+    ap.add_argument("--pid-dir", default=None, help="each rank writes its pid here")
     ap.add_argument("--nreduce", type=int, default=64)
     args = ap.parse_args()
     import torch.distributed as dist
@@ -28,6 +32,13 @@ def main():
     from tests.oracle_bridge import wc_ref
     from wcg import distributed as wd
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if args.pid_dir:
+        with open(os.path.join(args.pid_dir, f"rank{rank}.pid"), "w") as f:
+            f.write(str(os.getpid()))
+    if rank == args.ignore_term_rank:
+        import signal
+        signal.signal(signal.SIGTERM, signal.SIG_IGN)
+        time.sleep(3600)
     dist.init_process_group("gloo")
     if rank == args.fail_rank:
         raise SystemExit(7)

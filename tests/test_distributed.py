@@ -177,7 +177,7 @@ def _launch(nprocs, extra, timeout=120):
     return rc, buf.getvalue()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_launcher_runs_every_rank(world):
     """`bench.py --gpus N` without an external launcher: the parent starts N ranks (before any GPU
     call), relays rank 0's one JSON line and exits 0."""
@@ -202,6 +202,21 @@ def test_launcher_bounds_a_hung_rank():
     rc, out = _launch(2, ["--hang-rank", "1"], timeout=20)
     assert rc != 0
     assert time.time() - t0 < 60
+
+
+def test_launcher_kills_a_rank_that_ignores_sigterm(tmp_path):
+    """torch.distributed.run starts every rank in a session of its own, so a signal to
+    the launcher's process group alone does not reach them; a rank that ignores SIGTERM (stuck in
+    a driver call, or handling the signal) must still be gone when launch_ranks returns."""
+    import time
+    from wcg.launch import _alive
+    t0 = time.time()
+    rc, out = _launch(2, ["--ignore-term-rank", "1", "--pid-dir", str(tmp_path)], timeout=15)
+    assert rc != 0
+    assert time.time() - t0 < 90
+    pids = [int(open(os.path.join(tmp_path, f)).read()) for f in os.listdir(tmp_path)]
+    assert len(pids) == 2, pids
+    assert not [p for p in pids if _alive(p)], "a rank outlived the launcher"
 
 
 def test_bench_self_launches_before_any_gpu_call():
