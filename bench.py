@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--sync-steps", action="store_true",
+                    help="N = 1: every timed step waits for its reduce (wcg_reduce) instead of queuing the "
+                         "next job behind it (wcg_reduce_async)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N > 1 path with host-staged records, ranks may share a GPU")
     # below the driver's 600 s bench limit, so that the launcher's own bounded stop (and every
@@ -305,14 +308,19 @@ def main():
         import signal
         faulthandler.register(signal.SIGTERM, chain=True)
 
-    def step():
+    def step(pipelined=False):
         """one job: this rank's map (N = 1: + DoReduce and Merge; N > 1: + shuffle, owners'
-        DoReduce, Merge of the runs at rank 0)"""
+        DoReduce, Merge of the runs at rank 0).  pipelined (N = 1): the reduce is queued with its
+        size read-back and not waited for (wcg_reduce_async), so the host queues the next job
+        behind it and back-to-back jobs run without host gaps; each job still runs in full"""
         stage("map")
         eng.reset()
         eng.map_device(dev.data_ptr(), n)
         if world == 1:
-            eng.reduce()
+            if pipelined:
+                eng.reduce_async()
+            else:
+                eng.reduce()
             nstep[0] += 1
             return
         stage("exchange+reduce")
@@ -322,19 +330,24 @@ def main():
         stage("done")
         nstep[0] += 1
 
+    pipe = world == 1 and not args.sync_steps
     for _ in range(args.warmup):
-        step()
+        step(pipe)
+    if pipe:
+        eng.reduce_wait()
     eng.enable_timing(3)                      # a new epoch: the timed steps only
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # every step ends in a host wait (wcg_reduce reads back the formatted size; the N > 1 Merge is
-    # synchronous at root), so the host clock between steps times each step without extra work
+    # N > 1 (and --sync-steps): every step ends in a host wait (wcg_reduce reads back the formatted
+    # size; the N > 1 Merge is synchronous at root), so the host clock between steps times each step
     t0 = time.perf_counter()
     marks = [t0]
     for _ in range(args.steps):
-        step()
+        step(pipe)
         marks.append(time.perf_counter())
+    if pipe:
+        eng.reduce_wait()                     # the last job's sizes and status (errors surface here)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -344,9 +357,22 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if gloo else "cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    stats = eng.stats()
     map_sum, map_launches = eng.timings()         # k_map device ms, summed over the timed steps
     assert map_launches == args.steps, (map_launches, args.steps)
+    synced_ms = None
+    if pipe:
+        # the same K jobs with a host wait at the end of each (wcg_reduce): the per-step spread on
+        # the host clock, and the rate a caller that waits for every job sees
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        marks = [ts]
+        for _ in range(args.steps):
+            step(False)
+            marks.append(time.perf_counter())
+        torch.cuda.synchronize()
+        synced_ms = (time.perf_counter() - ts) / args.steps * 1e3
+        step_ms = [(b - a) * 1e3 for a, b in zip(marks, marks[1:])]
+    stats = eng.stats()
     # every phase (events around each), on instrumented steps after the timed region; N > 1 also
     # times the step's stages on the host clock with a synchronise after each (the shuffle through
     # gloo, host-staged, has no engine events; RCCL's wcg_exchange / wcg_gather_merge have them)
@@ -468,14 +494,27 @@ def main():
             return round(srt[min(len(srt) - 1, int(f * (len(srt) - 1) + 0.5))], 4)
         out["ms_per_step_median"] = q(0.5)
         out["ms_per_step_spread"] = {"min": q(0.0), "p10": q(0.1), "p90": q(0.9), "max": q(1.0),
-                                     "how": "host clock between steps (each step ends in a host wait); "
-                                            "value uses the mean over the bracketed loop"}
+                                     "how": ("host clock between the steps of a second K-step loop in which "
+                                             "every step waits for its reduce (wcg_reduce); value uses the "
+                                             "mean over the bracketed pipelined loop" if pipe else
+                                             "host clock between steps (each step ends in a host wait); "
+                                             "value uses the mean over the bracketed loop")}
+        out["step_mode"] = ("pipelined: reset, map, wcg_reduce_async per job, back to back on one stream; "
+                            "the last job's read-back waited for inside the timed region" if pipe else
+                            "synchronous: each job ends in its reduce's host read-back")
+        if synced_ms is not None:
+            out["ms_per_step_host_synced"] = round(synced_ms, 4)
+            out["value_host_synced"] = round(all_bytes / (synced_ms * 1e-3) / 1e9, 3)
         out["value_at_median_step"] = round(all_bytes / (q(0.5) * 1e-3) / 1e9, 3)
         out["stats"] = stats
         out["phase_ms_avg"] = {k: round(v / psteps, 4) for k, v in ph_sum.items()
                                if world > 1 or k in ("map", "agg", "compact", "sort", "format")}
         out["phase_timing"] = (f"HIP events around every phase on {psteps} instrumented steps after the "
                                "timed region (the timed steps carry events around k_map only)")
+        if world == 1:
+            fused = eng.reduce_path() == 1
+            out["reduce_path"] = ("one launch (csrc/wcg_fused.h): compaction, sort and formatting in one "
+                                  "persistent kernel, reported as phase 'sort'" if fused else "multi-launch")
         if world > 1:
             # the N > 1 step by phase (device time on each rank's work stream, HIP events):
             # map/agg/compact/sort/format = the rank's own map + its owners' DoReduce;

@@ -100,6 +100,18 @@ WCG_API int wcg_map_file(wcg_ctx *ctx, const char *path, uint64_t *mapped_bytes,
  * format the merged file "key: count\n".  Synchronous; returns key count and byte size. */
 WCG_API int wcg_reduce(wcg_ctx *ctx, uint64_t *nkeys, uint64_t *nbytes);
 
+/* The same job without the host wait: the reduce is queued on the context's stream (with the
+ * read-back of its sizes and error flags) and the call returns at once, so a host can queue the
+ * next job's wcg_reset / wcg_map* behind it (back-to-back jobs then run without host gaps).
+ * wcg_reduce_wait returns what wcg_reduce would have (sizes, or the job's error); every call that
+ * reads the job's results (wcg_result_*, wcg_partition*, wcg_export*, wcg_stats, wcg_timings,
+ * wcg_sync, the collectives) waits for it first.  A job not waited for before the next wcg_reset
+ * / wcg_map* / wcg_import is dropped, its results and its error status with it.  Jobs that take
+ * the multi-launch reduce (the first job of a context, large or two-pass jobs) are reduced
+ * synchronously here as by wcg_reduce. */
+WCG_API int wcg_reduce_async(wcg_ctx *ctx);
+WCG_API int wcg_reduce_wait(wcg_ctx *ctx, uint64_t *nkeys, uint64_t *nbytes);
+
 /* Device pointer to / host copy of the formatted output of the last wcg_reduce(). */
 WCG_API int wcg_result_device(wcg_ctx *ctx, const void **dev_ptr, uint64_t *nbytes);
 WCG_API int wcg_result_copy(wcg_ctx *ctx, uint8_t *host_out, uint64_t cap);
@@ -238,6 +250,11 @@ WCG_API int wcg_enable_timing(wcg_ctx *ctx, int on);
  * tokens > 15 bytes, long-key heap bytes (keys > 32 bytes; shorter long keys live in their
  * table slot's cell), overflow, spin_fail, records emitted by the second aggregation pass}. */
 WCG_API int wcg_stats(wcg_ctx *ctx, uint64_t *stats9);
+
+/* Diagnostics: which reduce the last wcg_reduce ran: *path = 1 for the one-launch reduce of small
+ * one-pass jobs (compaction, sort and formatting in one persistent kernel: jobs after the first of
+ * a context whose previous job had at most 2^17 keys), 0 for the multi-launch path. */
+WCG_API int wcg_reduce_path(const wcg_ctx *ctx, int *path);
 
 /* FNV-1a 32 (= ihash, mapreduce.go:185-189), host side, for partition arithmetic. */
 WCG_API uint32_t wcg_ihash(const uint8_t *key, uint64_t len);

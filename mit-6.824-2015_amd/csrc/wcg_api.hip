@@ -28,6 +28,7 @@
 #include "wcg_map.h"
 #include "wcg_agg.h"
 #include "wcg_reduce.h"
+#include "wcg_fused.h"
 #include "wcg_ingest.h"
 
 using namespace wcg;
@@ -153,6 +154,13 @@ struct wcg_ctx {
     std::vector<std::tuple<int, hipEvent_t, hipEvent_t>> xev;
     double acc[10] = {};                      // mode 2: phases folded in from recycled events
     u64 map_launches = 0;
+    // r05: the one-launch reduce of small one-pass jobs (wcg_fused.h): bucket regions, the spill
+    // list, sample runs, bucket counts / starts / byte flags and the control block, one allocation
+    uint8_t* fr_buf = nullptr;
+    FrArgs fr{};                              // the buffers' pointers (set once)
+    u32 fr_epoch = 0;
+    bool fused_last = false;                  // the last wcg_reduce took that path (diagnostics)
+    bool pending = false;                     // wcg_reduce_async queued a job not yet read back
     std::string err;
 };
 
@@ -343,6 +351,93 @@ int compact(wcg_ctx* c, bool defer = false) {
     c->crec = c->recA;
     c->compacted = true;
     return WCG_OK;
+}
+
+// One-launch reduce (wcg_fused.h) of a one-pass job: when the previous job of the context had at
+// most FR_NMAX keys (the plan of the device-sized path, which this replaces for small jobs) and no
+// record log or import is involved.  WCG_FUSED=0 keeps the multi-launch path (A/B, tests).
+u64 merged_bound(wcg_ctx* c, u64 n, bool json);
+
+bool fused_eligible(wcg_ctx* c) {
+    static const char* env = getenv("WCG_FUSED");
+    static const bool exact_env = getenv("WCG_EXACT_REDUCE") != nullptr || getenv("WCG_SORT_TARGET") != nullptr;
+    if (env && atoi(env) == 0) return false;
+    return !c->compacted && !c->two_pass_used && !c->imported && !exact_env && c->nrec_hint >= 2 &&
+           c->nrec_hint <= FR_NMAX;
+}
+
+int reduce_fused(wcg_ctx* c) {
+    const u64 total = c->gslots + c->lslots;
+    RC(ensure_recs(c, total));
+    c->dev_sized = true;                          // merged_bound: the whole long-key heap
+    RC(ensure(c, &c->d_out, &c->out_cap, merged_bound(c, total, false) + 64));
+    if (!c->fr_buf) {
+        // one allocation: regions | spill records | spill buckets | samples | counts | starts |
+        // flags | control block (zeroed once; each launch's last workgroup re-zeroes its counters)
+        const u64 sz_reg = (u64)FR_BMAX * FR_RCAP * sizeof(Rec), sz_sp = total * sizeof(Rec),
+                  sz_sb = (total * sizeof(u32) + 255) & ~255ull, sz_smp = 2ull * FR_SMAX * sizeof(u64),
+                  sz_cnt = FR_BMAX * sizeof(u32), sz_bs = (FR_BMAX + 1) * sizeof(u64) + 248,
+                  sz_fl = FR_BMAX * sizeof(u64), sz_ctl = (sizeof(FrCtl) + 255) & ~255ull;
+        const u64 all = sz_reg + sz_sp + sz_sb + sz_smp + sz_cnt + sz_bs + sz_fl + sz_ctl;
+        HIPCHK(c, hipMalloc(&c->fr_buf, all));
+        HIPCHK(c, hipMemsetAsync(c->fr_buf, 0, all, c->stream));
+        uint8_t* q = c->fr_buf;
+        c->fr.reg = reinterpret_cast<Rec*>(q); q += sz_reg;
+        c->fr.spill = reinterpret_cast<Rec*>(q); q += sz_sp;
+        c->fr.spill_bid = reinterpret_cast<u32*>(q); q += sz_sb;
+        c->fr.smp = reinterpret_cast<u64*>(q); q += sz_smp;
+        c->fr.bcnt = reinterpret_cast<u32*>(q); q += sz_cnt;
+        c->fr.bstart = reinterpret_cast<u64*>(q); q += sz_bs;
+        c->fr.bflag = reinterpret_cast<u64*>(q); q += sz_fl;
+        c->fr.ctl = reinterpret_cast<FrCtl*>(q);
+        c->fr.spill_cap = total;
+    }
+    // compaction counts into nrec / nlong: zero after wcg_reset and after a one-pass k_agg
+    if (!c->counts_clean) HIPCHK(c, hipMemsetAsync(&c->st->nrec, 0, 2 * sizeof(u64), c->stream));
+    c->counts_clean = false;
+    FrArgs a = c->fr;
+    a.gtab = c->gtab; a.gslots = c->gslots; a.ltab = c->ltab; a.lslots = c->lslots;
+    a.arena = c->arena; a.st = c->st; a.total_out = c->d_scalar;
+    a.rec = c->recA; a.rec_cap = c->rec_cap; a.out_rec = c->recB; a.out = c->d_out;
+    c->fr_epoch = (c->fr_epoch + 1) & 0xFFFFFF;
+    if (c->fr_epoch == 0) c->fr_epoch = 1;
+    a.epoch = c->fr_epoch;
+    const char* tenv = getenv("WCG_FUSED_TARGET");             // tests: records per bucket
+    a.target = tenv ? (u32)std::max(1, atoi(tenv)) : FR_TARGET;
+    a.nitems0 = (u32)cdiv(total, (u64)CP_NT * CP_IPT);
+    if (c->timing_all) { c->phase_ev[2] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream)); }
+    k_fused_reduce<<<(unsigned)(2 * c->ncu), FR_NT, 0, c->stream>>>(a);
+    HIPCHK(c, hipGetLastError());
+    if (c->timing_all) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }
+    // the job's one host round trip: counters, errors and the formatted size in one copy (waited
+    // for by reduce_fused_finish: at once in wcg_reduce, later after wcg_reduce_async)
+    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, ST_SCALAR_OFF + 9 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    c->dev_sized = false;
+    c->compacted = false;                         // recA is the fused launch's scratch
+    c->fused_last = true;
+    return WCG_OK;
+}
+
+// the job's results on the host: waits for the read-back of reduce_fused
+int reduce_fused_finish(wcg_ctx* c) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->sorted = c->recB;
+    c->crec = c->recA;
+    c->nrec = c->nkeys = c->h_st->nrec;
+    c->out_len = *c->h_scalar;
+    if (c->h_st->bad_input || c->h_st->overflow || c->h_st->spin_fail) {
+        c->nrec = 0; c->out_len = 0; c->reduced = false;
+        RC(check_status(c));                      // the error message (nothing was compacted)
+    }
+    c->nrec_hint = c->nrec;
+    return WCG_OK;
+}
+
+// a wcg_reduce_async job's results, before anything that reads them
+int resolve(wcg_ctx* c) {
+    if (!c->pending) return WCG_OK;
+    c->pending = false;
+    return reduce_fused_finish(c);
 }
 
 // WCG_DEBUG=1: synchronise and report after each stage of the rarely used paths (diagnostics)
@@ -849,7 +944,7 @@ int wcg_close(wcg_ctx* c) {
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
                     c->llog, c->llog_len, c->smp, c->bid, c->spx, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->ovf, c->hist, c->spart, c->ikey, c->iidx, c->groups,
                     c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig,
-                    c->d_xrow, c->xrecv, c->grecv, c->glist, c->llist};
+                    c->d_xrow, c->xrecv, c->grecv, c->glist, c->llist, c->fr_buf};
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_x) (void)hipHostFree(c->h_x);
@@ -1024,6 +1119,7 @@ extern "C" {
 
 int wcg_reset(wcg_ctx* c) {
     if (!c) return WCG_EINVAL;
+    c->pending = false;                 // a wcg_reduce_async job not waited for is dropped
     int rc = set_dev(c);
     if (rc) return rc;
     if (c->timing_mode >= 2 && c->ev_used >= EV_FOLD) {   // recycle the events of earlier jobs
@@ -1046,6 +1142,7 @@ int wcg_reset(wcg_ctx* c) {
 
 int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     if (!c) return WCG_EINVAL;
+    c->pending = false;
     if (n == 0) return WCG_OK;
     if (!dev_bytes || ((uintptr_t)dev_bytes & 15)) { c->err = "wcg_map_device: input must be 16-byte aligned"; return WCG_EINVAL; }
     int rc = set_dev(c);
@@ -1285,6 +1382,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
 
 int wcg_map(wcg_ctx* c, const uint8_t* host_bytes, uint64_t n) {
     if (!c) return WCG_EINVAL;
+    c->pending = false;
     if (n == 0) return WCG_OK;
     if (!host_bytes) return WCG_EINVAL;
     int rc = set_dev(c);
@@ -1295,6 +1393,7 @@ int wcg_map(wcg_ctx* c, const uint8_t* host_bytes, uint64_t n) {
 
 int wcg_map_file(wcg_ctx* c, const char* path, uint64_t* mapped_bytes, uint64_t* file_bytes) {
     if (!c || !path) return WCG_EINVAL;
+    c->pending = false;
     int rc = set_dev(c);
     if (rc) return rc;
     const int fd = open(path, O_RDONLY);
@@ -1323,6 +1422,25 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
     int rc = set_dev(c);
     if (rc) return rc;
     c->phase_ev[0] = c->phase_ev[1] = nullptr;     // set by compact() only when it runs now
+    RC(resolve(c));
+    c->fused_last = false;
+    if (fused_eligible(c)) {
+        rc = reduce_fused(c);
+        if (!rc) rc = reduce_fused_finish(c);
+        if (rc) return rc;
+        if (c->timing_all) {                       // the fused launch counts as the sort phase
+            c->phase_ev[4] = c->phase_ev[3];
+            c->phase_rec = true;
+            if (c->timing_mode == 2)
+                c->phase_jobs.push_back({c->phase_ev[0], c->phase_ev[1], c->phase_ev[2], c->phase_ev[3], c->phase_ev[4]});
+        }
+        c->reduced = true;
+        c->merged = false;
+        c->part_R = 0;
+        if (nkeys) *nkeys = c->nkeys;
+        if (nbytes) *nbytes = c->out_len;
+        return WCG_OK;
+    }
     RC(compact(c, true));
     c->merged = false;
     // sort + format; a device-sized job that fails in them leaves no capacity-sized record count
@@ -1367,8 +1485,42 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
     return WCG_OK;
 }
 
+int wcg_reduce_async(wcg_ctx* c) {
+    if (!c) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    RC(resolve(c));
+    if (!fused_eligible(c)) return wcg_reduce(c, nullptr, nullptr);   // the other paths read back at once
+    c->phase_ev[0] = c->phase_ev[1] = nullptr;
+    c->fused_last = false;
+    RC(reduce_fused(c));
+    if (c->timing_all) {
+        c->phase_ev[4] = c->phase_ev[3];
+        c->phase_rec = true;
+        if (c->timing_mode == 2)
+            c->phase_jobs.push_back({c->phase_ev[0], c->phase_ev[1], c->phase_ev[2], c->phase_ev[3], c->phase_ev[4]});
+    }
+    c->pending = true;
+    c->reduced = true;
+    c->merged = false;
+    c->part_R = 0;
+    return WCG_OK;
+}
+
+int wcg_reduce_wait(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
+    if (!c) return WCG_EINVAL;
+    if (!c->reduced) { c->err = "wcg_reduce_wait without a wcg_reduce_async job"; return WCG_ESTATE; }
+    int rc = set_dev(c);
+    if (rc) return rc;
+    RC(resolve(c));
+    if (nkeys) *nkeys = c->nkeys;
+    if (nbytes) *nbytes = c->out_len;
+    return WCG_OK;
+}
+
 int wcg_result_device(wcg_ctx* c, const void** dev_ptr, uint64_t* nbytes) {
     if (!c) return WCG_EINVAL;
+    RC(resolve(c));
     if (!c->reduced) { c->err = "wcg_result_device before wcg_reduce"; return WCG_ESTATE; }
     if (dev_ptr) *dev_ptr = c->d_out;
     if (nbytes) *nbytes = c->out_len;
@@ -1399,6 +1551,7 @@ int wcg_free(wcg_ctx* c, const void* dev_ptr) {
 
 int wcg_result_copy(wcg_ctx* c, uint8_t* host_out, uint64_t cap) {
     if (!c) return WCG_EINVAL;
+    RC(resolve(c));
     if (!c->reduced) { c->err = "wcg_result_copy before wcg_reduce"; return WCG_ESTATE; }
     if (cap < c->out_len) { c->err = "wcg_result_copy: buffer too small"; return WCG_EINVAL; }
     int rc = set_dev(c);
@@ -1412,6 +1565,7 @@ int wcg_result_copy(wcg_ctx* c, uint8_t* host_out, uint64_t cap) {
 
 int wcg_result_copy_device(wcg_ctx* c, void* dev_dst) {
     if (!c) return WCG_EINVAL;
+    RC(resolve(c));
     if (!c->reduced) { c->err = "wcg_result_copy_device before wcg_reduce"; return WCG_ESTATE; }
     int rc = set_dev(c);
     if (rc) return rc;
@@ -1421,6 +1575,7 @@ int wcg_result_copy_device(wcg_ctx* c, void* dev_dst) {
 
 int wcg_sync(wcg_ctx* c) {
     if (!c) return WCG_EINVAL;
+    RC(resolve(c));
     int rc = set_dev(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1429,6 +1584,7 @@ int wcg_sync(wcg_ctx* c) {
 
 int wcg_partition_all(wcg_ctx* c, uint32_t nreduce, uint8_t* host_out, uint64_t cap, uint64_t* part_bytes) {
     if (!c) return WCG_EINVAL;
+    RC(resolve(c));
     if (!c->reduced) { c->err = "wcg_partition_all before wcg_reduce"; return WCG_ESTATE; }
     if (c->merged) { c->err = "wcg_partition_all after wcg_merge_runs (a merged file has no partitions)"; return WCG_ESTATE; }
     if (nreduce == 0) { c->err = "wcg_partition_all: nreduce 0"; return WCG_EINVAL; }
@@ -1452,6 +1608,7 @@ int wcg_partition_all(wcg_ctx* c, uint32_t nreduce, uint8_t* host_out, uint64_t 
 
 int wcg_partition(wcg_ctx* c, uint32_t nreduce, uint32_t r, uint8_t* host_out, uint64_t cap, uint64_t* nbytes) {
     if (!c) return WCG_EINVAL;
+    RC(resolve(c));
     if (!c->reduced) { c->err = "wcg_partition before wcg_reduce"; return WCG_ESTATE; }
     if (c->merged) { c->err = "wcg_partition after wcg_merge_runs (a merged file has no partitions)"; return WCG_ESTATE; }
     if (nreduce == 0 || r >= nreduce) { c->err = "wcg_partition: bad partition"; return WCG_EINVAL; }
@@ -1474,6 +1631,7 @@ int wcg_partition(wcg_ctx* c, uint32_t nreduce, uint32_t r, uint8_t* host_out, u
 
 int wcg_export_count(wcg_ctx* c, uint32_t nreduce, uint32_t nranks, uint64_t* counts) {
     if (!c || !counts || nreduce == 0 || nranks == 0 || nranks > EX_MAX_RANKS) return WCG_EINVAL;
+    RC(resolve(c));
     if (c->merged) { c->err = "wcg_export after wcg_merge_runs"; return WCG_ESTATE; }
     int rc = set_dev(c);
     if (rc) return rc;
@@ -1526,6 +1684,7 @@ int wcg_export(wcg_ctx* c, uint32_t nreduce, uint32_t nranks, const void** dev_r
 
 int wcg_import(wcg_ctx* c, const void* dev_records, uint64_t nrecords) {
     if (!c) return WCG_EINVAL;
+    c->pending = false;
     if (nrecords == 0) return WCG_OK;
     if (!dev_records) return WCG_EINVAL;
     int rc = set_dev(c);
@@ -1544,6 +1703,7 @@ int wcg_import(wcg_ctx* c, const void* dev_records, uint64_t nrecords) {
 int wcg_merge_runs(wcg_ctx* c, const void* dev_text, const uint64_t* run_bytes, uint32_t nruns, uint64_t* nkeys,
                    uint64_t* nbytes) {
     if (!c || (nruns && !run_bytes)) return WCG_EINVAL;
+    c->pending = false;
     int rc = set_dev(c);
     if (rc) return rc;
     u64 total = 0;
@@ -1860,8 +2020,9 @@ int wcg_exchange(wcg_ctx* c, uint32_t nreduce, uint64_t* sent, uint64_t* receive
     const u32 W = (u32)c->comm_world, me = (u32)c->comm_rank;
     const u64 S = W + X_HDR;
     hipEvent_t e0 = mark(c);
-    int mine = WCG_OK;
-    if (nreduce == 0) { c->err = "wcg_exchange: nreduce 0"; mine = WCG_EINVAL; }
+    int mine = resolve(c);              // (a failed wcg_reduce_async job still joins the collectives)
+    if (mine) {}
+    else if (nreduce == 0) { c->err = "wcg_exchange: nreduce 0"; mine = WCG_EINVAL; }
     else if (c->merged) { c->err = "wcg_exchange after wcg_merge_runs"; mine = WCG_ESTATE; }
     HIPCHK(c, hipMemsetAsync(c->d_xrow + X_HDR, 0, W * sizeof(u64), c->stream));
     if (!mine) mine = x_count(c, nreduce, W, c->d_xrow + X_HDR);
@@ -1921,8 +2082,8 @@ int wcg_gather_merge(wcg_ctx* c, int root, uint64_t* nkeys, uint64_t* nbytes) {
     const bool am_root = c->comm_rank == root;
     const u64 S = 3;
     hipEvent_t e0 = mark(c);
-    int mine = WCG_OK;
-    if (!c->reduced || c->merged) { c->err = "wcg_gather_merge needs a wcg_reduce result"; mine = WCG_ESTATE; }
+    int mine = resolve(c);
+    if (!mine && (!c->reduced || c->merged)) { c->err = "wcg_gather_merge needs a wcg_reduce result"; mine = WCG_ESTATE; }
     u64* hdr = c->h_x;
     hdr[0] = (u64)mine; hdr[1] = mine ? 0 : c->out_len; hdr[2] = c->grecv ? c->grecv_cap : 0;
     HIPCHK(c, hipMemcpyAsync(c->d_xrow, hdr, S * sizeof(u64), hipMemcpyHostToDevice, c->stream));
@@ -1972,6 +2133,7 @@ int wcg_exchange_local(wcg_ctx** cs, uint32_t W, uint32_t nreduce, uint64_t* sen
     for (u32 p = 0; p < W; p++) {
         if (!cs[p]) return WCG_EINVAL;
         for (u32 q = 0; q < p; q++) if (cs[q] == cs[p]) return WCG_EINVAL;
+        RC(resolve(cs[p]));
         if (cs[p]->merged) { cs[p]->err = "wcg_exchange_local after wcg_merge_runs"; return WCG_ESTATE; }
     }
     std::vector<u64> m((u64)W * W);
@@ -2019,6 +2181,7 @@ int wcg_gather_merge_local(wcg_ctx** cs, uint32_t W, uint32_t root, uint64_t* nk
     std::vector<uint64_t> sizes(W), off(W);
     for (u32 p = 0; p < W; p++) {
         if (!cs[p]) return WCG_EINVAL;
+        RC(resolve(cs[p]));
         if (!cs[p]->reduced || cs[p]->merged) { cs[p]->err = "wcg_gather_merge_local needs a wcg_reduce result"; return WCG_ESTATE; }
         sizes[p] = cs[p]->out_len;
     }
@@ -2040,6 +2203,7 @@ int wcg_gather_merge_local(wcg_ctx** cs, uint32_t W, uint32_t root, uint64_t* nk
 
 int wcg_timings(wcg_ctx* c, double* ms, int n, uint64_t* map_launches) {
     if (!c || !ms || n < 0) return WCG_EINVAL;
+    RC(resolve(c));
     int rc = set_dev(c);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2062,8 +2226,15 @@ int wcg_timings(wcg_ctx* c, double* ms, int n, uint64_t* map_launches) {
     return WCG_OK;
 }
 
+int wcg_reduce_path(const wcg_ctx* c, int* path) {
+    if (!c || !path) return WCG_EINVAL;
+    *path = c->fused_last ? 1 : 0;
+    return WCG_OK;
+}
+
 int wcg_stats(wcg_ctx* c, uint64_t* s8) {   // 9 values (include/wcg.h)
     if (!c || !s8) return WCG_EINVAL;
+    RC(resolve(c));
     int rc = set_dev(c);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));

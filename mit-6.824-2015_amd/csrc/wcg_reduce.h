@@ -24,10 +24,11 @@ constexpr int CP_NT = 256, CP_IPT = 8;          // 2048 table slots per block, o
 // per-slot branch made a serial chain of memory latencies), then long keys' 16-byte prefixes.
 // glist (two-pass jobs): the gtab part is the gslots listed slots gtab[glist[i]], not gtab[0, gslots);
 // llist (large contexts): the ltab part is the lslots listed slots ltab[llist[i]]
-__global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
-                                                  const uint8_t* arena, Rec* out, u64 cap, DevState* st, u64* zero,
-                                                  const u64* glist, const u64* llist = nullptr) {
-    if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;   // a later kernel's counter
+// block `blk` of CP_NT * CP_IPT slots (a CP_NT-thread workgroup; k_compact and the fused reduce's
+// compaction phase, wcg_fused.h).  Workgroup-uniform early return only.
+__device__ __forceinline__ void compact_block(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
+                                              const uint8_t* arena, Rec* out, u64 cap, DevState* st,
+                                              const u64* glist, const u64* llist, u64 blk) {
     __shared__ u32 wsum[CP_NT / 64], wlong[CP_NT / 64];
     __shared__ u64 base_s;
     // a failed job (full table or arena, malformed import) compacts nothing: its slots may hold
@@ -36,7 +37,7 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
     if (st->overflow | st->spin_fail | st->bad_input) return;
     const u64 total = gslots + lslots;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const u64 b0 = (u64)blockIdx.x * CP_NT * CP_IPT;
+    const u64 b0 = blk * CP_NT * CP_IPT;
     GEntry e[CP_IPT];
 #pragma unroll
     for (int j = 0; j < CP_IPT; j++) {
@@ -95,6 +96,13 @@ __global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslot
 #pragma unroll
     for (int j = 0; j < CP_IPT; j++)
         if (have & (1u << j)) { if (pos < cap) out[pos] = r[j]; pos++; }   // more: host grows, reruns
+}
+
+__global__ __launch_bounds__(CP_NT) void k_compact(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
+                                                  const uint8_t* arena, Rec* out, u64 cap, DevState* st, u64* zero,
+                                                  const u64* glist, const u64* llist = nullptr) {
+    if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;   // a later kernel's counter
+    compact_block(gtab, gslots, ltab, lslots, arena, out, cap, st, glist, llist, blockIdx.x);
 }
 
 // wcg_reset: zero n1 + n2 16-byte words of two tables and the DevState counters, one dispatch;

@@ -26,7 +26,8 @@ EXPORTED = [
     "wcg_version", "wcg_map_file", "wcg_partition_all", "wcg_map_json", "wcg_export_count",
     "wcg_export_write", "wcg_merge_runs", "wcg_result_copy_device", "wcg_sync", "wcg_free",
     "wcg_comm_id", "wcg_comm_init", "wcg_exchange", "wcg_gather_merge", "wcg_exchange_plan",
-    "wcg_gather_plan", "wcg_exchange_local", "wcg_gather_merge_local",
+    "wcg_gather_plan", "wcg_exchange_local", "wcg_gather_merge_local", "wcg_reduce_path",
+    "wcg_reduce_async", "wcg_reduce_wait",
 ]
 COMM_ID_BYTES = 128
 
@@ -84,6 +85,9 @@ def load() -> ctypes.CDLL:
         "wcg_gather_plan": (I, [PU64, U32, U32, PU64, PU64]),
         "wcg_exchange_local": (I, [ctypes.POINTER(P), U32, U32, PU64, PU64]),
         "wcg_gather_merge_local": (I, [ctypes.POINTER(P), U32, U32, PU64, PU64]),
+        "wcg_reduce_path": (I, [P, ctypes.POINTER(I)]),
+        "wcg_reduce_async": (I, [P]),
+        "wcg_reduce_wait": (I, [P, PU64, PU64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -208,6 +212,16 @@ class Engine:
     def reduce(self) -> Tuple[int, int]:
         nk, nb = ctypes.c_uint64(), ctypes.c_uint64()
         self._chk(self._lib.wcg_reduce(self._ctx, ctypes.byref(nk), ctypes.byref(nb)))
+        return nk.value, nb.value
+
+    def reduce_async(self) -> None:
+        """wcg_reduce_async: queue the reduce (no host wait); reduce_wait() or any result call
+        waits for it, the next reset()/map_*() drops it."""
+        self._chk(self._lib.wcg_reduce_async(self._ctx))
+
+    def reduce_wait(self) -> Tuple[int, int]:
+        nk, nb = ctypes.c_uint64(), ctypes.c_uint64()
+        self._chk(self._lib.wcg_reduce_wait(self._ctx, ctypes.byref(nk), ctypes.byref(nb)))
         return nk.value, nb.value
 
     def result_device(self) -> Tuple[int, int]:
@@ -343,6 +357,12 @@ class Engine:
         nl = ctypes.c_uint64()
         self._chk(self._lib.wcg_timings(self._ctx, ms, 10, ctypes.byref(nl)))
         return dict(zip(self.PHASES, list(ms))), nl.value
+
+    def reduce_path(self) -> int:
+        """1 if the last reduce() ran the one-launch reduce (wcg_fused.h), 0 for the multi-launch one."""
+        v = ctypes.c_int()
+        self._chk(self._lib.wcg_reduce_path(self._ctx, ctypes.byref(v)))
+        return v.value
 
     def stats(self) -> dict:
         s = (ctypes.c_uint64 * 9)()
