@@ -90,10 +90,13 @@ def test_sizes(eng, nkeys, ntok, tie_every):
 
 
 def test_empty_and_letterless(eng):
+    """jobs of no key (after a job of 0 keys the hint is 0: the next job takes the general path)"""
     job(eng, corpus(100, 500, 4))
     check(eng, b"")
+    check(eng, corpus(100, 500, 5), fused=False)
     check(eng, b"... 123 !!\n")
-    check(eng, corpus(100, 500, 5))
+    job(eng, corpus(100, 500, 6))
+    check(eng, corpus(1, 1, 7))
 
 
 def test_tiny_buckets_many_runs(eng, target):
