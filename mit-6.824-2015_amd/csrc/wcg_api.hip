@@ -161,6 +161,7 @@ struct wcg_ctx {
     u32 fr_epoch = 0;
     bool fused_last = false;                  // the last wcg_reduce took that path (diagnostics)
     bool pending = false;                     // wcg_reduce_async queued a job not yet read back
+    u64* h_st_dev = nullptr;                  // h_st's device address (the fused launch writes it)
     std::string err;
 };
 
@@ -372,13 +373,16 @@ int reduce_fused(wcg_ctx* c) {
     c->dev_sized = true;                          // merged_bound: the whole long-key heap
     RC(ensure(c, &c->d_out, &c->out_cap, merged_bound(c, total, false) + 64));
     if (!c->fr_buf) {
-        // one allocation: regions | spill records | spill buckets | samples | counts | starts |
-        // flags | control block (zeroed once; each launch's last workgroup re-zeroes its counters)
-        const u64 sz_reg = (u64)FR_BMAX * FR_RCAP * sizeof(Rec), sz_sp = total * sizeof(Rec),
-                  sz_sb = (total * sizeof(u32) + 255) & ~255ull, sz_smp = 2ull * FR_SMAX * sizeof(u64),
-                  sz_cnt = FR_BMAX * sizeof(u32), sz_bs = (FR_BMAX + 1) * sizeof(u64) + 248,
-                  sz_fl = FR_BMAX * sizeof(u64), sz_ctl = (sizeof(FrCtl) + 255) & ~255ull;
-        const u64 all = sz_reg + sz_sp + sz_sb + sz_smp + sz_cnt + sz_bs + sz_fl + sz_ctl;
+        // one allocation: regions | spill records | spill buckets | samples and splitters | sample
+        // occupancy | counts | bytes | starts | offsets | control block (zeroed once; each launch's
+        // last workgroup re-zeroes its counters)
+        auto al = [](u64 x) { return (x + 255) & ~255ull; };
+        const u64 sz_reg = (u64)FR_BMAX * FR_RCAP * sizeof(Rec), sz_sp = al(total * sizeof(Rec)),
+                  sz_sb = al(total * sizeof(u32)), sz_smp = 4ull * FR_SMAX * sizeof(u64),
+                  sz_occ = al(FR_SMAX * sizeof(u32)), sz_cnt = al(FR_BMAX * sizeof(u32)),
+                  sz_by = al(FR_BMAX * sizeof(u64)), sz_bs = al((FR_BMAX + 1) * sizeof(u64)),
+                  sz_ctl = al(sizeof(FrCtl));
+        const u64 all = sz_reg + sz_sp + sz_sb + sz_smp + sz_occ + sz_cnt + sz_by + 2 * sz_bs + sz_ctl;
         HIPCHK(c, hipMalloc(&c->fr_buf, all));
         HIPCHK(c, hipMemsetAsync(c->fr_buf, 0, all, c->stream));
         uint8_t* q = c->fr_buf;
@@ -386,9 +390,11 @@ int reduce_fused(wcg_ctx* c) {
         c->fr.spill = reinterpret_cast<Rec*>(q); q += sz_sp;
         c->fr.spill_bid = reinterpret_cast<u32*>(q); q += sz_sb;
         c->fr.smp = reinterpret_cast<u64*>(q); q += sz_smp;
+        c->fr.socc = reinterpret_cast<u32*>(q); q += sz_occ;
         c->fr.bcnt = reinterpret_cast<u32*>(q); q += sz_cnt;
+        c->fr.bbytes = reinterpret_cast<u64*>(q); q += sz_by;
         c->fr.bstart = reinterpret_cast<u64*>(q); q += sz_bs;
-        c->fr.bflag = reinterpret_cast<u64*>(q); q += sz_fl;
+        c->fr.boff = reinterpret_cast<u64*>(q); q += sz_bs;
         c->fr.ctl = reinterpret_cast<FrCtl*>(q);
         c->fr.spill_cap = total;
     }
@@ -406,12 +412,77 @@ int reduce_fused(wcg_ctx* c) {
     a.target = tenv ? (u32)std::max(1, atoi(tenv)) : FR_TARGET;
     a.nitems0 = (u32)cdiv(total, (u64)CP_NT * CP_IPT);
     if (c->timing_all) { c->phase_ev[2] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[2], c->stream)); }
-    k_fused_reduce<<<(unsigned)(2 * c->ncu), FR_NT, 0, c->stream>>>(a);
+    static const bool fclock = getenv("WCG_FUSED_CLOCK") != nullptr;   // diagnostics: phase clocks
+    static u64* d_fclk = nullptr;
+    const unsigned fgrid = (unsigned)(2 * c->ncu);
+    a.clk = nullptr;
+    if (fclock) {
+        if (!d_fclk) HIPCHK(c, hipMalloc(&d_fclk, ((u64)fgrid * FR_CLK + 8ull * FR_NPH * FR_CLK_ITEMS + 8ull * FR_NPH) * sizeof(u64)));
+        HIPCHK(c, hipMemsetAsync(d_fclk, 0, ((u64)fgrid * FR_CLK + 8ull * FR_NPH * FR_CLK_ITEMS + 8ull * FR_NPH) * sizeof(u64), c->stream));
+        a.clk = d_fclk;
+    }
+    if (!c->h_st_dev) HIPCHK(c, hipHostGetDevicePointer((void**)&c->h_st_dev, c->h_st, 0));
+    a.host_st = c->h_st_dev;
+    k_fused_reduce<<<fgrid, FR_NT, 0, c->stream>>>(a);
     HIPCHK(c, hipGetLastError());
+    if (fclock) {
+        std::vector<u64> h((u64)fgrid * FR_CLK + 8ull * FR_NPH * FR_CLK_ITEMS + 8ull * FR_NPH);
+        HIPCHK(c, hipMemcpyAsync(h.data(), d_fclk, h.size() * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        u64 t0 = ~0ull, tend = 0;
+        for (unsigned w = 0; w < fgrid; w++) { t0 = std::min(t0, h[w * FR_CLK]); }
+        fprintf(stderr, "wcg fused clock (us from the first workgroup's start):");
+        for (int p = 0; p < FR_NPH; p++) {
+            u64 ent = ~0ull, first = ~0ull, lastfirst = 0, left = 0;
+            unsigned nw = 0;
+            for (unsigned w = 0; w < fgrid; w++) {
+                const u64* r = &h[w * FR_CLK];
+                if (r[1 + 3 * p]) ent = std::min(ent, r[1 + 3 * p]);
+                if (r[2 + 3 * p]) { first = std::min(first, r[2 + 3 * p]); lastfirst = std::max(lastfirst, r[2 + 3 * p]); nw++; }
+                left = std::max(left, r[3 + 3 * p]);
+            }
+            tend = std::max(tend, left);
+            fprintf(stderr, " | P%d entered %.1f first item %.1f last first item %.1f (%u wgs) all left %.1f", p,
+                    ent == ~0ull ? -1.0 : (ent - t0) / 100.0, first == ~0ull ? -1.0 : (first - t0) / 100.0,
+                    lastfirst ? (lastfirst - t0) / 100.0 : -1.0, nw, (left - t0) / 100.0);
+        }
+        u64 smax = 0;
+        for (unsigned w = 0; w < fgrid; w++) smax = std::max(smax, h[w * FR_CLK]);
+        fprintf(stderr, " | last wg start %.1f, end %.1f\n", (smax - t0) / 100.0, (tend - t0) / 100.0);
+        fprintf(stderr, "  publish (at / acquire, parameters, release us):");
+        for (int q = 1; q < FR_NPH; q++) {
+            const u64* k = &h[(u64)fgrid * FR_CLK + 8ull * FR_NPH * FR_CLK_ITEMS + 8 * q];
+            if (k[0] && k[3]) fprintf(stderr, " | P%d %.1f / %.1f %.1f %.1f", q, (k[0] - t0) / 100.0, (k[1] - k[0]) / 100.0,
+                                      (k[2] - k[1]) / 100.0, (k[3] - k[2]) / 100.0);
+        }
+        fprintf(stderr, "\n");
+        for (int p = 0; p < FR_NPH; p++) {      // per item: sub-steps, work, release, count (median / max, us)
+            std::vector<std::vector<double>> d(7);
+            for (u32 i = 0; i < FR_CLK_ITEMS; i++) {
+                const u64* q = &h[(u64)fgrid * FR_CLK + ((u64)p * FR_CLK_ITEMS + i) * 8];
+                if (!q[0] || !q[7]) continue;
+                u64 prev = q[0];
+                for (int k = 1; k < 8; k++) {
+                    if (!q[k]) { d[k - 1].push_back(0); continue; }
+                    d[k - 1].push_back((q[k] - prev) / 100.0);
+                    prev = q[k];
+                }
+            }
+            if (d[0].empty()) continue;
+            fprintf(stderr, "  P%d %zu items (med/max us): ", p, d[0].size());
+            const char* nm[7] = {"s1", "s2", "s3", "s4", "work", "release", "count"};
+            for (int k = 0; k < 7; k++) {
+                std::vector<double> v = d[k];
+                std::sort(v.begin(), v.end());
+                fprintf(stderr, "%s %.1f/%.1f  ", nm[k], v[v.size() / 2], v.back());
+            }
+            fprintf(stderr, "\n");
+        }
+    }
     if (c->timing_all) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }
-    // the job's one host round trip: counters, errors and the formatted size in one copy (waited
-    // for by reduce_fused_finish: at once in wcg_reduce, later after wcg_reduce_async)
-    HIPCHK(c, hipMemcpyAsync(c->h_st, c->st, ST_SCALAR_OFF + 9 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    // the job's one host round trip: counters, errors and the formatted size, written into the
+    // pinned host block by the launch's last workgroup (waited for by reduce_fused_finish: at once
+    // in wcg_reduce, later after wcg_reduce_async)
     c->dev_sized = false;
     c->compacted = false;                         // recA is the fused launch's scratch
     c->fused_last = true;

@@ -25,16 +25,21 @@ constexpr int CP_NT = 256, CP_IPT = 8;          // 2048 table slots per block, o
 // glist (two-pass jobs): the gtab part is the gslots listed slots gtab[glist[i]], not gtab[0, gslots);
 // llist (large contexts): the ltab part is the lslots listed slots ltab[llist[i]]
 // block `blk` of CP_NT * CP_IPT slots (a CP_NT-thread workgroup; k_compact and the fused reduce's
-// compaction phase, wcg_fused.h).  Workgroup-uniform early return only.
+// compaction phase, wcg_fused.h).  Workgroup-uniform early return only.  blk_count (the fused
+// reduce): the block's records go to out[blk * CP_NT * CP_IPT, ...) and their number to
+// blk_count[blk] (no shared counter: 320 returning atomics on DevState::nrec serialised)
 __device__ __forceinline__ void compact_block(const GEntry* gtab, u64 gslots, const GEntry* ltab, u64 lslots,
                                               const uint8_t* arena, Rec* out, u64 cap, DevState* st,
-                                              const u64* glist, const u64* llist, u64 blk) {
+                                              const u64* glist, const u64* llist, u64 blk, u32* blk_count = nullptr) {
     __shared__ u32 wsum[CP_NT / 64], wlong[CP_NT / 64];
     __shared__ u64 base_s;
     // a failed job (full table or arena, malformed import) compacts nothing: its slots may hold
     // half-published long keys (no arena offset), and the reduce's sort and formatting may run
     // before the host reads the error (device-sized jobs)
-    if (st->overflow | st->spin_fail | st->bad_input) return;
+    if (st->overflow | st->spin_fail | st->bad_input) {
+        if (blk_count && threadIdx.x == 0) blk_count[blk] = 0;
+        return;
+    }
     const u64 total = gslots + lslots;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u64 b0 = blk * CP_NT * CP_IPT;
@@ -49,10 +54,15 @@ __device__ __forceinline__ void compact_block(const GEntry* gtab, u64 gslots, co
         if (i >= total) e[j].k0 = 0;
     }
     uint4 q[CP_IPT];
+    if (b0 + (u64)CP_NT * CP_IPT > gslots) {          // (workgroup-uniform: a block of the global table
+#pragma unroll                                        // has no long key and skips this round trip)
+        for (int j = 0; j < CP_IPT; j++) {
+            const bool lng = b0 + (u64)j * CP_NT + tid >= gslots && e[j].k0 != 0;
+            q[j] = *reinterpret_cast<const uint4*>(arena + (lng ? e[j].k1 - 1 : 0));   // arena cells: 16-byte aligned
+        }
+    } else {
 #pragma unroll
-    for (int j = 0; j < CP_IPT; j++) {
-        const bool lng = b0 + (u64)j * CP_NT + tid >= gslots && e[j].k0 != 0;
-        q[j] = *reinterpret_cast<const uint4*>(arena + (lng ? e[j].k1 - 1 : 0));   // arena cells: 16-byte aligned
+        for (int j = 0; j < CP_IPT; j++) q[j] = make_uint4(0, 0, 0, 0);
     }
     Rec r[CP_IPT];
     u32 have = 0, nlong = 0;
@@ -88,7 +98,8 @@ __device__ __forceinline__ void compact_block(const GEntry* gtab, u64 gslots, co
     if (tid == 0) {
         u32 all = 0, al = 0;
         for (int k = 0; k < CP_NT / 64; k++) { const u32 v = wsum[k]; wsum[k] = all; all += v; al += wlong[k]; }
-        base_s = all ? atomicAdd(&st->nrec, (u64)all) : 0;
+        if (blk_count) { base_s = b0; blk_count[blk] = all; }
+        else base_s = all ? atomicAdd(&st->nrec, (u64)all) : 0;
         if (al) atomicAdd(&st->nlong, (u64)al);
     }
     __syncthreads();
