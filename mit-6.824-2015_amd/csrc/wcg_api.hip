@@ -449,6 +449,25 @@ int reduce_fused(wcg_ctx* c) {
         u64 smax = 0;
         for (unsigned w = 0; w < fgrid; w++) smax = std::max(smax, h[w * FR_CLK]);
         fprintf(stderr, " | last wg start %.1f, end %.1f\n", (smax - t0) / 100.0, (tend - t0) / 100.0);
+        for (int p = 1; p < FR_NPH; p++) {      // per workgroup: entry spread and what preceded the latest
+            std::vector<double> ent, fi;
+            double worst = -1, wprev = 0, went = 0;
+            for (unsigned w = 0; w < fgrid; w++) {
+                const u64* r = &h[w * FR_CLK];
+                if (r[1 + 3 * p]) ent.push_back((r[1 + 3 * p] - t0) / 100.0);
+                if (r[2 + 3 * p]) {
+                    const double f = (r[2 + 3 * p] - t0) / 100.0;
+                    fi.push_back(f);
+                    if (f > worst) { worst = f; wprev = (r[3 * p] - t0) / 100.0; went = (r[1 + 3 * p] - t0) / 100.0; }
+                }
+            }
+            if (ent.empty() || fi.empty()) continue;
+            std::sort(ent.begin(), ent.end());
+            std::sort(fi.begin(), fi.end());
+            auto qt = [](const std::vector<double>& v, double f) { return v[(size_t)(f * (v.size() - 1))]; };
+            fprintf(stderr, "  P%d entered q10/50/90/max %.1f %.1f %.1f %.1f; first item %.1f %.1f %.1f %.1f; latest: left P%d %.1f entered %.1f\n",
+                    p, qt(ent, .1), qt(ent, .5), qt(ent, .9), ent.back(), qt(fi, .1), qt(fi, .5), qt(fi, .9), fi.back(), p - 1, wprev, went);
+        }
         fprintf(stderr, "  publish (at / acquire, parameters, release us):");
         for (int q = 1; q < FR_NPH; q++) {
             const u64* k = &h[(u64)fgrid * FR_CLK + 8ull * FR_NPH * FR_CLK_ITEMS + 8 * q];

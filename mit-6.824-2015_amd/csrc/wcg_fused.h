@@ -23,10 +23,17 @@
 // every item of the phase before it has been taken (by running workgroups), so the launch cannot
 // deadlock whatever the residency: a workgroup that starts late finds no tickets and leaves.  The
 // workgroup that completes a phase's last item publishes the next phase's parameters (release
-// fence, then the phase's ready word = the launch's epoch); the others poll that word and acquire
-// (MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility": producer waves drain
-// their stores, a barrier, one lane's agent release; consumer: one poll, one agent acquire, a
-// barrier, plain loads).  The last workgroup to leave zeroes the counters for the next launch.
+// fence, then the phase's ready words = the launch's epoch | B << 32); the others poll a copy.
+// Visibility across the 8 XCDs (whose L2s are not coherent with each other):
+//   - items write what a later phase reads with write-through stores (fr_st: sc1) and drain them
+//     (vmcnt(0)) before they are counted; the publisher's own stores go out with its release;
+//   - consumers read with plain loads after the poll and take NO acquire.  An agent acquire is an
+//     L2 invalidate of the XCD (buffer_inv sc1): 64 workgroups per XCD invalidating in turn spread
+//     each phase's wake-up over ~4.5 us (r05 clock: entry q10-max 9.0-12.2 us with it, 7.8-8.2
+//     without).  No stale copy can be hit instead: the dispatch invalidates the caches at the
+//     launch's start, and no line a phase hands over (samples, splitters, bucket regions, spill
+//     list, bucket starts) is read by anyone in the launch before it is handed over.
+// The last workgroup to leave zeroes the counters for the next launch.
 //
 // Rare cases stay exact, only slower: a bucket past its region (FR_RCAP records: the sample put
 // too few splitters there, or the estimate of the key count was far off) is gathered from the spill
@@ -56,14 +63,22 @@ static_assert(FR_SMAX <= FR_CAP, "the sample is staged in the bucket sort's LDS 
 // counters and parameters, one 128-byte line each (the counters take every workgroup's atomics)
 constexpr u32 FR_SHARDS = 8;             // done counters per phase (workgroup % 8: one per XCD under
                                          // round-robin dispatch), then one top counter per phase
+// Words that many workgroups hit at once are spread over FR_SPREAD-byte strides (device-scope
+// atomics and polls are served one at a time per address at the memory side: 512 workgroups polling
+// one ready word woke over ~4.5 us, the last ones ~10 ns x 512 after the first).
+#ifndef FR_ENTRY_ACQUIRE
+#define FR_ENTRY_ACQUIRE 0      // 1: an agent acquire at every phase entry (measurement only)
+#endif
+constexpr u32 FR_SPREAD = 4096 / sizeof(u32);
+constexpr u32 FR_RCOPIES = 16;           // copies of each ready word; workgroup w polls w % 16
 struct FrCtl {
     u32 ticket[FR_NPH][32];
     u32 done[FR_NPH][32];                // top: shards completed
-    u32 dshard[FR_NPH][FR_SHARDS][32];   // items completed per shard
-    u32 ready[FR_NPH][32];               // = the launch's epoch once the phase's parameters are out
     u32 exits[32];
     u32 nspill[32];
     u64 B, pad[7];                       // parameters (plain stores before a ready word)
+    u32 dshard[FR_NPH][FR_SHARDS][FR_SPREAD];    // items completed per shard
+    u64 ready[FR_NPH][FR_RCOPIES][FR_SPREAD / 2];   // epoch | B << 32 once the phase's parameters are out
 };
 
 struct FrArgs {
@@ -694,7 +709,8 @@ FR_NOINLINE void fr_publish(int q) {
         if (pk) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); pk[2] = wall_clock64(); }
         fr_release_wg();
         if (pk) pk[3] = wall_clock64();
-        if (tid == 0) __hip_atomic_store(&C->ready[q][0], g.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid < FR_RCOPIES)               // (fr_sb = B in every publisher: set by the poll, or above)
+            __hip_atomic_store(&C->ready[q][tid][0], (u64)g.epoch | fr_sb << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         if (items) break;
     }
@@ -728,15 +744,21 @@ __global__ __launch_bounds__(FR_NT, 2) void k_fused_reduce(FrArgs a) {
         if (p > 0) {
             if (tid == 0) {
                 u32 spins = 0, f = 0;
-                while (fr_poll(&C->ready[p][0]) != g.epoch) {
+                u64 rw;
+                while ((u32)(rw = fr_poll64(&C->ready[p][blockIdx.x % FR_RCOPIES][0])) != g.epoch) {
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > FR_SPIN_LIMIT) { f = 1; atomicAdd((u32*)&g.st->spin_fail, 1u); break; }
                 }
                 fr_s_fail = f;
+                fr_sb = rw >> 32;
             }
+#if FR_ENTRY_ACQUIRE
             fr_acquire_wg();
+#else
+            __syncthreads();
+#endif
             if (fr_s_fail) { failed = true; break; }
-            B = C->B;
+            B = fr_sb;
         }
         if (clk) clk[1 + 3 * p] = wall_clock64();
         bool first_item = true;
@@ -744,6 +766,7 @@ __global__ __launch_bounds__(FR_NT, 2) void k_fused_reduce(FrArgs a) {
         for (bool first = true;; first = false) {
             // the first item of a phase is the workgroup's own number (512 workgroups taking a ticket
             // from one word at once queued 3-6 us); past the grid, tickets (counted from gridDim.x)
+            if (!first && nitems <= gridDim.x) break;     // (no ticketed items this phase)
             if (tid == 0 && !first) fr_s_item = gridDim.x + fr_add(&C->ticket[p][0], 1u);
             if (tid == 0 && first) fr_s_item = blockIdx.x;
             __syncthreads();
