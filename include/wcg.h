@@ -251,6 +251,15 @@ WCG_API int wcg_enable_timing(wcg_ctx *ctx, int on);
  * table slot's cell), overflow, spin_fail, records emitted by the second aggregation pass}. */
 WCG_API int wcg_stats(wcg_ctx *ctx, uint64_t *stats9);
 
+/* Diagnostics: the last wcg_map_file / wcg_map ingest, from its own timers and events (ms unless
+ * noted): out[0] host wall time until every chunk was issued, out[1] reading (pread + line scan)
+ * on the calling thread and its reader pool, out[2] waiting for a free staging slot, out[3] the
+ * chunks' H2D copies (sum of copy durations), out[4] the copy engine's span (first copy start to
+ * last copy end), out[5] its idle fraction 1 - out[3] / out[4], out[6] the chunks' map kernels
+ * (sum), out[7] device span from the first copy to the last chunk's map end, out[8] chunks.
+ * Waits for the context's streams.  n = number of doubles the caller provides (<= 9). */
+WCG_API int wcg_ingest_stats(wcg_ctx *ctx, double *out, int n);
+
 /* Diagnostics: which reduce the last wcg_reduce ran: *path = 1 for the one-launch reduce of small
  * one-pass jobs (compaction, sort and formatting in one persistent kernel: jobs after the first of
  * a context whose previous job had at most 2^17 keys), 0 for the multi-launch path. */

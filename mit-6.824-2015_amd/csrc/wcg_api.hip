@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -136,6 +137,11 @@ struct wcg_ctx {
     uint8_t* db[INGEST_SLOTS] = {};
     uint8_t* dbig = nullptr; u64 dbig_cap = 0;
     hipEvent_t ev_copied[INGEST_SLOTS] = {}, ev_mapped[INGEST_SLOTS] = {};
+    // the last ingest's own breakdown (wcg_ingest_stats): timing events around each chunk's copy
+    // (copy stream) and map kernels (work stream), four per chunk, kept for the context's life
+    std::vector<hipEvent_t> ing_ev;
+    double ing[3] = {};                       // host: issue wall, reading, waiting for a slot (ms)
+    u64 ing_chunks = 0;
     hipStream_t copy_stream = nullptr;
     std::unique_ptr<TaskPool> readers;
     u64 ingest_bytes = 0;                     // bytes mapped by the last wcg_map / wcg_map_file
@@ -807,6 +813,17 @@ int partition_all(wcg_ctx* c, u32 R) {
 }
 
 // ---------------------------------------------------------------- ingest
+// the ingest's timing events for chunk k: [4k] copy start, [4k + 1] copy end, [4k + 2] map start,
+// [4k + 3] map end
+int ingest_events(wcg_ctx* c, u64 k) {
+    while (c->ing_ev.size() < 4 * (k + 1)) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        c->ing_ev.push_back(e);
+    }
+    return WCG_OK;
+}
+
 int ingest_init(wcg_ctx* c) {
     if (c->hb[0]) return WCG_OK;
     // measurement knobs: chunk bytes (default 64 MiB) and reader threads (default min(16, cores))
@@ -844,30 +861,53 @@ int ingest(wcg_ctx* c, u64 size, const std::function<void(uint8_t*, u64, u64)>& 
     // thread goes on reading the next chunk meanwhile.  The context belongs to the issuer while
     // chunks are queued; this thread touches it again only after drain().
     std::string ierr;
+    using clk = std::chrono::steady_clock;
+    const auto t_start = clk::now();
+    double read_ms = 0, wait_ms = 0;
+    u64 nchunk = 0;                                   // chunks issued (the issuer's count)
     Issuer issuer([&](int s, u64 cut) -> int {
         if (hipSetDevice(c->device) != hipSuccess) { ierr = "hipSetDevice (ingest issuer)"; return WCG_EHIP; }
+        if (ingest_events(c, nchunk)) { ierr = c->err; return WCG_EHIP; }
+        hipEvent_t* ev = &c->ing_ev[4 * nchunk];
+        nchunk++;
         hipError_t e = hipStreamWaitEvent(c->copy_stream, c->ev_mapped[s], 0);   // device slot free
+        if (e == hipSuccess) e = hipEventRecord(ev[0], c->copy_stream);
         if (e == hipSuccess) e = hipMemcpyAsync(c->db[s], c->hb[s], cut, hipMemcpyHostToDevice, c->copy_stream);
+        if (e == hipSuccess) e = hipEventRecord(ev[1], c->copy_stream);
         if (e == hipSuccess) e = hipEventRecord(c->ev_copied[s], c->copy_stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_copied[s], 0);
+        if (e == hipSuccess) e = hipEventRecord(ev[2], c->stream);
         if (e != hipSuccess) { ierr = std::string("ingest copy: ") + hipGetErrorString(e); return WCG_EHIP; }
         const int rc = wcg_map_device(c, c->db[s], cut);
         if (rc) return rc;
-        e = hipEventRecord(c->ev_mapped[s], c->stream);
+        e = hipEventRecord(ev[3], c->stream);
+        if (e == hipSuccess) e = hipEventRecord(c->ev_mapped[s], c->stream);
         if (e == hipSuccess) e = hipEventSynchronize(c->ev_copied[s]);       // the staging buffer is free
         if (e != hipSuccess) { ierr = std::string("ingest copy: ") + hipGetErrorString(e); return WCG_EHIP; }
         return WCG_OK;
     });
+    // the host side of the breakdown, once every chunk is issued (the device side is read from
+    // the chunks' events by wcg_ingest_stats, so the ingest itself never waits for them)
+    auto breakdown = [&]() {
+        c->ing[0] = std::chrono::duration<double, std::milli>(clk::now() - t_start).count();
+        c->ing[1] = read_ms;
+        c->ing[2] = wait_ms;
+        c->ing_chunks = nchunk;
+    };
     auto drain = [&]() -> int {
         const int rc = issuer.drain();
         if (rc && !ierr.empty()) c->err = ierr;
+        if (!rc) breakdown();
         return rc;
     };
     while (true) {
         {
+            const auto tw = clk::now();
             const int rc = issuer.wait_slot(slot);                    // staging slot free
+            wait_ms += std::chrono::duration<double, std::milli>(clk::now() - tw).count();
             if (rc) { (void)drain(); if (!ierr.empty()) c->err = ierr; return rc; }
         }
+        const auto tr = clk::now();
         uint8_t* h = c->hb[slot];
         if (carry) memmove(h, c->hb[(slot + INGEST_SLOTS - 1) % INGEST_SLOTS] + cut_prev, carry);
         // the staging buffers hold chunk + SCAN_MAX_LINE bytes (a split-mode carry is < 64 KiB; a
@@ -884,6 +924,7 @@ int ingest(wcg_ctx* c, u64 size, const std::function<void(uint8_t*, u64, u64)>& 
                 if (split_mode) sl[t] = scan_slice(h, (int64_t)a, (int64_t)b);
             });
         }
+        read_ms += std::chrono::duration<double, std::milli>(clk::now() - tr).count();
         const u64 len = carry + want;
         fo += want;
         const bool eof = fo == size;
@@ -1026,6 +1067,7 @@ int wcg_close(wcg_ctx* c) {
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < INGEST_SLOTS; i++) {
         if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
+    for (auto e : c->ing_ev) (void)hipEventDestroy(e);
         if (c->ev_mapped[i]) (void)hipEventDestroy(c->ev_mapped[i]);
         if (c->hb[i]) (void)hipHostFree(c->hb[i]);
         if (c->db[i]) (void)hipFree(c->db[i]);
@@ -1504,6 +1546,36 @@ int wcg_map_file(wcg_ctx* c, const char* path, uint64_t* mapped_bytes, uint64_t*
     if (ioerr) { c->err = "wcg_map_file: read error"; return WCG_EHIP; }
     if (mapped_bytes) *mapped_bytes = c->ingest_bytes;
     if (file_bytes) *file_bytes = size;
+    return WCG_OK;
+}
+
+int wcg_ingest_stats(wcg_ctx* c, double* out, int n) {
+    if (!c || !out || n < 0) return WCG_EINVAL;
+    int rc = set_dev(c);
+    if (rc) return rc;
+    RC(resolve(c));
+    double copy = 0, map = 0, span = 0, dev = 0;
+    const u64 nk = c->ing_chunks;
+    if (nk) {
+        HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const hipEvent_t* ev = c->ing_ev.data();
+        for (u64 k = 0; k < nk; k++) {
+            float a = 0, b = 0;
+            HIPCHK(c, hipEventElapsedTime(&a, ev[4 * k], ev[4 * k + 1]));
+            HIPCHK(c, hipEventElapsedTime(&b, ev[4 * k + 2], ev[4 * k + 3]));
+            copy += a;
+            map += b;
+        }
+        float sp = 0, dv = 0;
+        HIPCHK(c, hipEventElapsedTime(&sp, ev[0], ev[4 * (nk - 1) + 1]));
+        HIPCHK(c, hipEventElapsedTime(&dv, ev[0], ev[4 * (nk - 1) + 3]));
+        span = sp;
+        dev = dv;
+    }
+    const double st[9] = {c->ing[0], c->ing[1], c->ing[2], copy, span, span > 0 ? std::max(0.0, 1.0 - copy / span) : 0.0,
+                          map, dev, (double)nk};
+    for (int i = 0; i < n && i < 9; i++) out[i] = st[i];
     return WCG_OK;
 }
 

@@ -27,7 +27,7 @@ EXPORTED = [
     "wcg_export_write", "wcg_merge_runs", "wcg_result_copy_device", "wcg_sync", "wcg_free",
     "wcg_comm_id", "wcg_comm_init", "wcg_exchange", "wcg_gather_merge", "wcg_exchange_plan",
     "wcg_gather_plan", "wcg_exchange_local", "wcg_gather_merge_local", "wcg_reduce_path",
-    "wcg_reduce_async", "wcg_reduce_wait",
+    "wcg_reduce_async", "wcg_reduce_wait", "wcg_ingest_stats",
 ]
 COMM_ID_BYTES = 128
 
@@ -88,6 +88,7 @@ def load() -> ctypes.CDLL:
         "wcg_reduce_path": (I, [P, ctypes.POINTER(I)]),
         "wcg_reduce_async": (I, [P]),
         "wcg_reduce_wait": (I, [P, PU64, PU64]),
+        "wcg_ingest_stats": (I, [P, ctypes.POINTER(ctypes.c_double), I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -363,6 +364,17 @@ class Engine:
         v = ctypes.c_int()
         self._chk(self._lib.wcg_reduce_path(self._ctx, ctypes.byref(v)))
         return v.value
+
+    INGEST_STATS = ["host_issue_ms", "read_ms", "slot_wait_ms", "copy_ms", "copy_span_ms",
+                    "copy_engine_idle_frac", "map_ms", "device_span_ms", "chunks"]
+
+    def ingest_stats(self) -> dict:
+        """The last map_file / map_host ingest's breakdown (wcg_ingest_stats): host reading and
+        slot waits, the chunks' H2D copies and the copy engine's idle share of its span, the
+        chunks' map kernels, and the device span from the first copy to the last map."""
+        v = (ctypes.c_double * len(self.INGEST_STATS))()
+        self._chk(self._lib.wcg_ingest_stats(self._ctx, v, len(self.INGEST_STATS)))
+        return dict(zip(self.INGEST_STATS, list(v)))
 
     def stats(self) -> dict:
         s = (ctypes.c_uint64 * 9)()

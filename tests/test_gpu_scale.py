@@ -4,6 +4,7 @@
     table, one per token and in runs that straddle 16-byte chunks, against the C oracle;
   * C4's key cardinality: the first GiB of the C4 generator (2.4e7 distinct keys) through
     several wcg_map_device calls into one context sized for 5e7 keys;
+  * the 64 GiB job's call size: 16 GiB of C4 in two 8 GiB calls, verified exactly;
   * a C3-shaped job: 2 GiB of the C3 generator, nReduce = 64, all 64 -res-<r> files.
 """
 import pytest
@@ -107,6 +108,51 @@ def test_c4_4gib_sixteen_calls_record_log_overflow(c4_gen):
     assert st["emitted"] > 50_000_000 + 65536 and st["global_ops"] > 0 and st["overflow"] == 0
     print(f"c4 4 GiB: {nk} keys, {st['emitted']} records emitted; verifying", flush=True)
     ok, msg, ntok, nkeys = ob.verify_merged(host.ctypes.data, n, got, 16)
+    assert ok, msg
+    assert ntok == st["tokens"] and nkeys == nk
+
+
+@pytest.mark.timeout(600)
+def test_c4_16gib_two_8gib_calls(c4_gen):
+    """The 64 GiB job's call size (tools/c4_full.py: 8 GiB per wcg_map_device) at a quarter of its
+    length: 16 GiB of the C4 generator in two 8 GiB calls into one 5e7-key context.  Each call's
+    pass 2 emits more records than the record log holds, so the second call's records go to the
+    global table and the reduce merges log and table.  Checked exactly by the oracle's verifier
+    (every input token decrements its line's count; keys strictly ascending).  ~2 minutes: 25 s
+    to generate, a few s on the GPU, ~70 s to verify on 16 threads."""
+    import threading
+    import time
+    import numpy as np
+    import torch
+    import wcg
+    from wcg.corpus import BLOCK
+    n, q, gib = 16 << 30, 8 << 30, 1 << 30
+    host = np.empty(n, dtype=np.uint8)
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for g in range(n // gib):
+        a = g * gib
+        c4_gen.fill_ptr(host.ctypes.data + a, gib, first_block=a // BLOCK, threads=16)
+        dev[a:a + gib].copy_(torch.from_numpy(host[a:a + gib]))
+    torch.cuda.synchronize()
+    print("c4 16 GiB: generated", flush=True)
+    with wcg.Engine(0, 0, 50_000_000) as e:
+        e.reset()
+        for k in range(n // q):
+            e.map_device(dev.data_ptr() + k * q, q)
+        nk, _ = e.reduce()
+        got = e.result()
+        st = e.stats()
+    del dev
+    assert st["emitted"] > 50_000_000 and st["global_ops"] > 0 and st["overflow"] == 0 and nk > 20_000_000
+    print(f"c4 16 GiB: {nk} keys, {st['emitted']} records emitted; verifying", flush=True)
+    res = {}
+    th = threading.Thread(target=lambda: res.update(v=ob.verify_merged(host.ctypes.data, n, got, 16)), daemon=True)
+    t0 = time.perf_counter()
+    th.start()
+    while th.is_alive():
+        th.join(20)
+        print(f"c4 16 GiB: verifying ({time.perf_counter() - t0:.0f} s)", flush=True)
+    ok, msg, ntok, nkeys = res["v"]
     assert ok, msg
     assert ntok == st["tokens"] and nkeys == nk
 
