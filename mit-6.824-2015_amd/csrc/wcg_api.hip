@@ -494,12 +494,12 @@ int reduce_fused(wcg_ctx* c) {
                 }
             }
             if (d[0].empty()) continue;
-            fprintf(stderr, "  P%d %zu items (med/max us): ", p, d[0].size());
+            fprintf(stderr, "  P%d %zu items (med/p90/max us): ", p, d[0].size());
             const char* nm[7] = {"s1", "s2", "s3", "s4", "work", "release", "count"};
             for (int k = 0; k < 7; k++) {
                 std::vector<double> v = d[k];
                 std::sort(v.begin(), v.end());
-                fprintf(stderr, "%s %.1f/%.1f  ", nm[k], v[v.size() / 2], v.back());
+                fprintf(stderr, "%s %.1f/%.1f/%.1f  ", nm[k], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
             }
             fprintf(stderr, "\n");
         }

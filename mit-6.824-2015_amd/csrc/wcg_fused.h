@@ -535,9 +535,12 @@ FR_NOINLINE void fr_scatter_item(u64 item, u64 B, bool load_sp, FR_G u64* ick) {
 
 // the bucket's register network by size class (a call each: the 8-entry class alone needs more
 // registers than the rest)
+#ifndef FR_SORT_CMP
+#define FR_SORT_CMP 1           // 0: the (hi, lo) network only (no compressed-word pass)
+#endif
 template <int E>
 FR_NOINLINE void fr_bucket_sort(const FR_G Rec* X, u32 m) {
-    sb_sort_regs<FR_NT, E>((const Rec*)X, m, fr_kh, fr_kl, fr_kp, E < 8 ? true : (bool)WCG_SORT_HIONLY_BIG);
+    sb_sort_regs<FR_NT, E>((const Rec*)X, m, fr_kh, fr_kl, fr_kp, FR_SORT_CMP && (E < 8 ? true : (bool)WCG_SORT_HIONLY_BIG));
 }
 
 // the lines of x[0, 8) with lengths L (0: none) at dst + lo: staged in LDS and written out in
@@ -638,7 +641,8 @@ FR_NOINLINE void fr_bucket_item(u32 b, FR_G u64* ick) {
     }
     if (m == 0) return;                                   // (workgroup-uniform)
     const FR_G Rec* const X = g.reg + (u64)b * FR_RCAP;
-    if (m <= FR_NT) fr_bucket_sort<1>(X, (u32)m);
+    if (m <= FR_NT) fr_bucket_sort<1>(X, (u32)m);   // (a rank sort - every record against all
+                                                      // in LDS - measured 2x slower at 256: r05)
     else if (m <= 2 * FR_NT) fr_bucket_sort<2>(X, (u32)m);
     else if (m <= 4 * FR_NT) fr_bucket_sort<4>(X, (u32)m);
     else fr_bucket_sort<8>(X, (u32)m);
