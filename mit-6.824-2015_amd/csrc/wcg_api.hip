@@ -483,9 +483,16 @@ int reduce_fused(wcg_ctx* c) {
         fprintf(stderr, "\n");
         for (int p = 0; p < FR_NPH; p++) {      // per item: sub-steps, work, release, count (median / max, us)
             std::vector<std::vector<double>> d(7);
+            std::vector<std::pair<double, u64>> slow;      // P3: (item time, bucket size)
             for (u32 i = 0; i < FR_CLK_ITEMS; i++) {
-                const u64* q = &h[(u64)fgrid * FR_CLK + ((u64)p * FR_CLK_ITEMS + i) * 8];
+                u64 q[8];
+                std::copy(&h[(u64)fgrid * FR_CLK + ((u64)p * FR_CLK_ITEMS + i) * 8],
+                          &h[(u64)fgrid * FR_CLK + ((u64)p * FR_CLK_ITEMS + i) * 8] + 8, q);
                 if (!q[0] || !q[7]) continue;
+                if (q[3] >> 62 == 1) {
+                    slow.push_back({(q[7] - q[0]) / 100.0, q[3] & ~(1ull << 62)});
+                    q[3] = 0;
+                }
                 u64 prev = q[0];
                 for (int k = 1; k < 8; k++) {
                     if (!q[k]) { d[k - 1].push_back(0); continue; }
@@ -502,6 +509,13 @@ int reduce_fused(wcg_ctx* c) {
                 fprintf(stderr, "%s %.1f/%.1f/%.1f  ", nm[k], v[v.size() / 2], v[v.size() * 9 / 10], v.back());
             }
             fprintf(stderr, "\n");
+            if (!slow.empty()) {
+                std::sort(slow.begin(), slow.end());
+                fprintf(stderr, "  P%d slowest items (us, records):", p);
+                for (size_t k = slow.size() > 6 ? slow.size() - 6 : 0; k < slow.size(); k++)
+                    fprintf(stderr, " %.1f/%llu", slow[k].first, (unsigned long long)slow[k].second);
+                fprintf(stderr, "; median item %.1f/%llu\n", slow[slow.size() / 2].first, (unsigned long long)slow[slow.size() / 2].second);
+            }
         }
     }
     if (c->timing_all) { c->phase_ev[3] = take_event(c); HIPCHK(c, hipEventRecord(c->phase_ev[3], c->stream)); }

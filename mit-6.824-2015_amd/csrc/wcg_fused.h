@@ -538,8 +538,21 @@ FR_NOINLINE void fr_scatter_item(u64 item, u64 B, bool load_sp, FR_G u64* ick) {
 #ifndef FR_SORT_CMP
 #define FR_SORT_CMP 1           // 0: the (hi, lo) network only (no compressed-word pass)
 #endif
+#ifndef FR_ABL_SORT
+#define FR_ABL_SORT 0           // diagnostics (wrong order): 1 = the bucket's loads only, no network
+#endif
 template <int E>
 FR_NOINLINE void fr_bucket_sort(const FR_G Rec* X, u32 m) {
+    if (FR_ABL_SORT) {
+        for (u32 i = threadIdx.x; i < m; i += FR_NT) {
+            const uint4 v = *reinterpret_cast<const FR_G uint4*>(X + i);
+            fr_kh[i] = (u64)v.y << 32 | v.x;
+            fr_kl[i] = (u64)v.w << 32 | v.z;
+            fr_kp[i] = (uint16_t)i;
+        }
+        __syncthreads();
+        return;
+    }
     sb_sort_regs<FR_NT, E>((const Rec*)X, m, fr_kh, fr_kl, fr_kp, FR_SORT_CMP && (E < 8 ? true : (bool)WCG_SORT_HIONLY_BIG));
 }
 
@@ -641,6 +654,7 @@ FR_NOINLINE void fr_bucket_item(u32 b, FR_G u64* ick) {
     }
     if (m == 0) return;                                   // (workgroup-uniform)
     const FR_G Rec* const X = g.reg + (u64)b * FR_RCAP;
+    if (ick) ick[3] = m | 1ull << 62;                     // (the clock report's bucket size)
     if (m <= FR_NT) fr_bucket_sort<1>(X, (u32)m);   // (a rank sort - every record against all
                                                       // in LDS - measured 2x slower at 256: r05)
     else if (m <= 2 * FR_NT) fr_bucket_sort<2>(X, (u32)m);
