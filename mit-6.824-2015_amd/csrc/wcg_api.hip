@@ -68,6 +68,7 @@ struct wcg_ctx {
     // read-back, and the sort is planned for the previous job's count (nrec_hint)
     bool dev_sized = false;
     u64 nrec_hint = 0;
+    u64 long_hint = ~0ull;                    // long tokens of the previous job (unknown: ~0)
     // DevState's nrec / nlong are zero on the device: wcg_reset cleared them, or a one-pass
     // k_agg did, and no compaction has counted into them since (a second wcg_reduce
     // without a map in between would otherwise append to the first one's count)
@@ -540,6 +541,7 @@ int reduce_fused_finish(wcg_ctx* c) {
         RC(check_status(c));                      // the error message (nothing was compacted)
     }
     c->nrec_hint = c->nrec;
+    c->long_hint = c->h_st->long_tokens;
     return WCG_OK;
 }
 
@@ -855,6 +857,9 @@ int ingest_init(wcg_ctx* c) {
     c->readers.reset(new TaskPool((int)nr));
     return WCG_OK;
 }
+
+// long tokens of the previous job up to which a one-pass map call runs k_long_small
+constexpr u64 LONG_SMALL_MAX = 4096;
 
 // a byte after which no rune and no token continues: an ASCII byte that is not a letter
 inline bool safe_cut_byte(uint8_t b) { return b < 0x80 && ((b | 0x20) - 'a') >= 26u; }
@@ -1431,7 +1436,14 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
         HIPCHK(c, hipStreamWaitEvent(c->long_stream, c->ev_fork, 0));
     }
-    if (long_path) {
+    // one-pass calls after a job with few long tokens: one small workgroup does it all
+    static const char* ls_env = getenv("WCG_LONG_SMALL");        // measurement: 0 = never, 1 = always
+    const bool small = long_path && !two_pass && grid <= LS_MAXREG &&
+                       (ls_env ? atoi(ls_env) != 0 : c->long_hint <= LONG_SMALL_MAX);
+    if (small) {
+        k_long_small<<<1, LS_NT, 0, ls>>>(a, (u32)grid);
+        HIPCHK(c, hipGetLastError());
+    } else if (long_path) {
         LongPart lp;
         const u64 expect = grid * (u64)a.tiles_per_wg * 16;     // 16 per step: 3x C4's rate
         lp.cap = (u32)std::min<u64>(std::max<u64>(1024, (expect * 5 / 4 + LQ - 1) / LQ), 0x7FFFFFFFull);
@@ -1642,6 +1654,7 @@ int wcg_reduce(wcg_ctx* c, uint64_t* nkeys, uint64_t* nbytes) {
         }
     }
     c->nrec_hint = c->nrec;
+    if (c->h_st) c->long_hint = c->h_st->long_tokens;     // (a hint: read back with the sizes)
     if (c->timing_all) {
         c->phase_ev[4] = take_event(c);
         HIPCHK(c, hipEventRecord(c->phase_ev[4], c->stream));

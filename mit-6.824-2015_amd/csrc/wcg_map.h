@@ -736,6 +736,106 @@ __global__ __launch_bounds__(LA_NT) void k_long_agg(MapArgs a, LongPart lp) {
     }
 }
 
+// k_long_small: the long-key work of a one-pass map call with few long tokens, in ONE workgroup
+// (C2 logs ~200 long tokens per GiB; k_long_hash + k_long_agg, a 1024-workgroup and a
+// 256-workgroup launch that nearly all find nothing to do, took 17.5 us per step: r05 trace).
+// Rounds of LS_NT logged tokens over every region (a region found by binary search over the
+// regions' prefix in LDS): each token is walked if its length was left open, hashed from the
+// input, and claims or finds its tag's LDS slot (the claimer's occurrence is the slot's
+// representative); after a barrier it is compared with the representative (bytes 0-31 in LDS, the
+// rest from the input) and counted there.  Then every slot is added to the long-key table once,
+// unfenced: this workgroup is the table's only writer in the launch (as a partition's workgroup is
+// in k_long_agg).  Exact for any number of tokens: a tag collision or a full LDS table falls back to
+// a fenced insert of that occurrence; more tokens only take more rounds.
+constexpr int LS_NT = 1024;
+constexpr u32 LS_SLOTS = 2048;
+constexpr u32 LS_MAXREG = LS_NT;              // map regions (one length per thread)
+__global__ __launch_bounds__(LS_NT) void k_long_small(MapArgs a, u32 nreg) {
+    __shared__ u64 stag[LS_SLOTS], srec[LS_SLOTS], scnt[LS_SLOTS];
+    __shared__ uint4 sw[LS_SLOTS][2];
+    __shared__ u32 rpre[LS_MAXREG + 1];
+    __shared__ u32 ls_ws[LS_NT / 64];
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (u32 s = tid; s < LS_SLOTS; s += LS_NT) { stag[s] = 0; srec[s] = 0; scnt[s] = 0; }
+    // the regions' record counts (clamped to the log: a fuller region was flagged by k_map) and
+    // their exclusive prefix
+    u32 cnt = tid < nreg ? a.llog_len[tid] : 0u;
+    cnt = cnt < a.llog_cap ? cnt : a.llog_cap;
+    u32 incl = cnt;
+    for (int d = 1; d < 64; d <<= 1) { const u32 y = __shfl_up(incl, d, 64); if (lane >= (u32)d) incl += y; }
+    if (lane == 63) ls_ws[wv] = incl;
+    __syncthreads();
+    u32 pre = 0, total = 0;
+    for (u32 v = 0; v < LS_NT / 64; v++) { if (v < wv) pre += ls_ws[v]; total += ls_ws[v]; }
+    if (tid <= nreg) rpre[tid] = tid < nreg ? pre + incl - cnt : total;
+    __syncthreads();
+    for (u32 base = 0; base < total; base += LS_NT) {
+        const u32 i = base + tid;
+        u64 p = 0, len = 0, h = 0;
+        u32 w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (i < total) {
+            u32 lo = 0, hi = nreg;                    // the region: the last r with rpre[r] <= i
+            while (hi - lo > 1) {
+                const u32 mid = (lo + hi) >> 1;
+                if (rpre[mid] <= i) lo = mid; else hi = mid;
+            }
+            const u64 r = a.llog[(u64)lo * a.llog_cap + (i - rpre[lo])];
+            p = r & LLOG_OFF_MASK;
+            len = r >> 40;
+            if (len == 0) {                           // a run to measure (length 0 in the log)
+                u64 L = long_walk(a, p);
+                if (L <= 15) { count_inline_run(a, p, L); L = 0; }
+                else if (L > LONG_LEN_MAX) { atomicAdd(&a.st->overflow, 1u); L = 0; }
+                len = L;
+            }
+            if (len) h = input_lhash(a, p, (u32)len, w);
+        }
+        const bool valid = len != 0;
+        const u64 tag = valid ? long_tag(h, len) : 0;
+        int slot = -1;
+        if (valid) {
+            const u32 s0 = (u32)(tag >> 8) & (LS_SLOTS - 1);
+            for (u32 j = 0; j < LA_PROBES; j++) {
+                const u32 s = (s0 + j) & (LS_SLOTS - 1);
+                u64 t = stag[s];
+                if (t == 0) {
+                    t = atomicCAS((unsigned long long*)&stag[s], 0ull, (unsigned long long)tag);
+                    if (t == 0) {
+                        srec[s] = p | len << 40;
+                        sw[s][0] = make_uint4(w[0], w[1], w[2], w[3]);
+                        sw[s][1] = make_uint4(w[4], w[5], w[6], w[7]);
+                        slot = (int)s;
+                        break;
+                    }
+                }
+                if (t == tag) { slot = (int)s; break; }
+            }
+        }
+        __syncthreads();                              // representatives written
+        bool fallback = valid && slot < 0;
+        if (valid && slot >= 0) {
+            const u64 rr = srec[slot];
+            if ((rr >> 40) == len && w8_same(w, sw[slot][0], sw[slot][1]) &&
+                long_rest_same(a, p, rr & LLOG_OFF_MASK, (u32)len))
+                atomicAdd((unsigned long long*)&scnt[slot], 1ull);
+            else fallback = true;
+        }
+        if (fallback) {
+            atomicAdd(&a.st->long_fb, 1u);
+            ltab_add(a, len, tag, long_words(a, p, len, w), 1, true);
+        }
+        __syncthreads();                              // (as in k_long_agg: no slot of the next round
+    }                                                 // is confused with this round's representatives)
+    for (u32 s = tid; s < LS_SLOTS; s += LS_NT) {
+        const u64 c = scnt[s];
+        if (c == 0) continue;
+        const u64 rr = srec[s], len = rr >> 40, p = rr & LLOG_OFF_MASK;
+        const uint4 x = sw[s][0], y = sw[s][1];
+        const u32 w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+        ltab_add(a, len, stag[s], long_words(a, p, len, w), c, false);
+    }
+}
+
 // wave-local ordering of LDS accesses between lanes (the LDS executes one wave's
 // instructions in order; this keeps the compiler from moving accesses across)
 __device__ __forceinline__ void wave_lds_sync() {
