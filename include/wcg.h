@@ -193,7 +193,12 @@ WCG_API int wcg_export_write(wcg_ctx *ctx, void *dev_dst);
  * Collective calls: every rank of the communicator makes them in the same order.  A rank that
  * fails before data moves (a full table: WCG_EFULL; a call out of order; an allocation) still
  * joins the collectives with its status, and then EVERY rank returns an error (no rank is left
- * waiting in a send or receive); no units have moved and the tables are as they were. */
+ * waiting in a send or receive); no units have moved and the tables are as they were.  A device
+ * fault (a sticky HIP error: the context's stream can run nothing more, collectives included) is
+ * outside this contract: that rank cannot join, its peers wait in the collective until the job is
+ * stopped (bench.py's launcher stops every rank after --launch-timeout).  wcg_exchange_local
+ * applies the same agreement across its contexts (tests/test_gpu_exchange_local.py forces a full
+ * table on one of them). */
 #define WCG_COMM_ID_BYTES 128
 WCG_API int wcg_comm_id(uint8_t *id_out /* WCG_COMM_ID_BYTES */);
 WCG_API int wcg_comm_init(wcg_ctx *ctx, const uint8_t *id /* WCG_COMM_ID_BYTES */, int rank, int world);

@@ -2322,19 +2322,32 @@ int wcg_exchange_local(wcg_ctx** cs, uint32_t W, uint32_t nreduce, uint64_t* sen
     for (u32 p = 0; p < W; p++) {
         if (!cs[p]) return WCG_EINVAL;
         for (u32 q = 0; q < p; q++) if (cs[q] == cs[p]) return WCG_EINVAL;
-        RC(resolve(cs[p]));
-        if (cs[p]->merged) { cs[p]->err = "wcg_exchange_local after wcg_merge_runs"; return WCG_ESTATE; }
     }
+    // every context's status and counts first, as wcg_exchange's all-gather carries them: a
+    // context that fails locally (a full table, a failed wcg_reduce_async job, a call out of order)
+    // fails the exchange on every context, with no data moved and every table untouched
     std::vector<u64> m((u64)W * W);
+    std::vector<u64> status(W, 0);
     for (u32 p = 0; p < W; p++) {
         wcg_ctx* c = cs[p];
-        RC(set_dev(c));
-        RC(x_buffers(c, W));
-        HIPCHK(c, hipMemsetAsync(c->d_xrow + X_HDR, 0, W * sizeof(u64), c->stream));
-        RC(x_count(c, nreduce, W, c->d_xrow + X_HDR));
-        HIPCHK(c, hipMemcpyAsync(x_hmat(c), c->d_xrow + X_HDR, W * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        std::copy(x_hmat(c), x_hmat(c) + W, m.begin() + (u64)p * W);
+        status[p] = (u64)[&]() -> int {
+            RC(resolve(c));
+            if (c->merged) { c->err = "wcg_exchange_local after wcg_merge_runs"; return WCG_ESTATE; }
+            RC(set_dev(c));
+            RC(x_buffers(c, W));
+            HIPCHK(c, hipMemsetAsync(c->d_xrow + X_HDR, 0, W * sizeof(u64), c->stream));
+            RC(x_count(c, nreduce, W, c->d_xrow + X_HDR));
+            HIPCHK(c, hipMemcpyAsync(x_hmat(c), c->d_xrow + X_HDR, W * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            std::copy(x_hmat(c), x_hmat(c) + W, m.begin() + (u64)p * W);
+            return WCG_OK;
+        }();
+    }
+    for (u32 p = 0; p < W; p++) {
+        if (!status[p]) continue;
+        for (u32 q = 0; q < W; q++)
+            if (!status[q]) (void)x_statuses(cs[q], status.data(), 1, W, WCG_OK, "wcg_exchange_local");
+        return (int)status[p];
     }
     std::vector<u64> roff((u64)W * W), ts(W), tr(W);
     for (u32 p = 0; p < W; p++) {

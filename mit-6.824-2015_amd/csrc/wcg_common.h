@@ -429,6 +429,24 @@ __device__ __forceinline__ void list_claim(DevState* st, u64 which, u64* counter
     }
 }
 
+// THE claim of an empty table slot (CAS k0: 0 -> key) and, when it succeeds, its entry in the
+// table's claim list (large contexts clear and compact only the listed slots: a claim that skipped
+// the list would survive wcg_reset and drop out of compaction).  Every insert path claims through
+// these two: ginsert, ltab_add (k_long_*, fallbacks), k_import.  On failure *seen
+// holds the slot's current k0.
+__device__ __forceinline__ bool gtab_claim(DevState* st, GEntry* e, u64 s, u64 key, u64* seen) {
+    *seen = 0;
+    if (!cas_agent(&e->k0, seen, key)) return false;
+    list_claim(st, ST_GLIST, &st->gnew, GLIST_CAP, s);
+    return true;
+}
+__device__ __forceinline__ bool ltab_claim(DevState* st, GEntry* e, u64 s, u64 tag, u64* seen) {
+    *seen = 0;
+    if (!cas_agent(&e->k0, seen, tag)) return false;
+    list_claim(st, ST_LLIST, &st->lnew, LLIST_CAP, s);
+    return true;
+}
+
 // Insert/accumulate an inline key into the global table (open addressing, linear probing from
 // slot_hash).  Claim protocol: CAS k0 0 -> key; a key of 8+ bytes then publishes k1 (never 0).
 // A reader that sees k0 == key but k1 == 0 re-reads in a later iteration (the claimer publishes
@@ -442,14 +460,13 @@ __device__ __forceinline__ void ginsert(GEntry* tab, u64 mask, u64 k0, u64 k1, u
         GEntry* e = &tab[s];
         u64 c0 = ld_agent(&e->k0);
         if (c0 == 0) {
-            u64 exp = 0;
-            if (cas_agent(&e->k0, &exp, k0)) {
+            u64 exp;
+            // (two-pass contexts keep the global table nearly empty - a few fallback inserts per
+            // GiB - and list its claimed slots, so that compaction and wcg_reset visit those slots
+            // instead of the whole GB-sized table)
+            if (gtab_claim(st, e, s, k0, &exp)) {
                 if (!shrt) st_agent(&e->k1, k1);
                 add_agent(&e->cnt, cnt);
-                // two-pass contexts keep the global table nearly empty (a few fallback inserts per
-                // GiB) and list its claimed slots, so that compaction and wcg_reset visit those
-                // slots instead of the whole (GB-sized) table
-                list_claim(st, ST_GLIST, &st->gnew, GLIST_CAP, s);
                 return;
             }
             c0 = exp;

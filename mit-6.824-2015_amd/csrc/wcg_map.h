@@ -173,9 +173,8 @@ __device__ __forceinline__ u64 ltab_add(const MapArgs& a, u64 len, u64 tag, W w,
         u64 r = ld_agent(&e->k1);
         u64 elen = ld_agent(&e->aux);
         if (c0 == 0) {
-            u64 exp = 0;
-            if (cas_agent(&e->k0, &exp, tag)) {
-                list_claim(a.st, ST_LLIST, &a.st->lnew, LLIST_CAP, s);
+            u64 exp;
+            if (ltab_claim(a.st, e, s, tag, &exp)) {
                 const u64 off = long_home(s, len, a.lmask + 1, a.arena_cap, &a.st->arena_top);
                 if (off == ~0ull) { atomicAdd(&a.st->overflow, 1u); return 0; }
                 const u64 cells = long_cells(len);

@@ -657,9 +657,8 @@ __global__ void k_import(const Rec* in, u64 n, GEntry* gtab, u64 gmask, GEntry* 
             GEntry* e = &ltab[s];
             u64 c0 = ld_agent(&e->k0);
             if (c0 == 0) {
-                u64 exp = 0;
-                if (cas_agent(&e->k0, &exp, tag)) {
-                    list_claim(st, ST_LLIST, &st->lnew, LLIST_CAP, s);
+                u64 exp;
+                if (ltab_claim(st, e, s, tag, &exp)) {
                     const u64 off = long_home(s, len, lmask + 1, arena_cap, &st->arena_top);
                     if (off == ~0ull) { atomicAdd(&st->overflow, 1u); break; }
                     const u64 cells = long_cells(len);

@@ -1043,7 +1043,12 @@ __global__ void k_ss_colscan(u32* hist, u32 B, u32 G, u32* bstart) {
 // key more than once: the global table, other map calls, pass 2's overflow) are merged while a
 // bucket is written out: the first record of a run takes the run's total and the others count 0,
 // which formats to no line (wcg_reduce.h: line_len).  An inline key's 16-byte prefix is the whole
-// key (byte 15 is 0; a long key's is a letter byte), and long keys are never repeated.
+// key (byte 15 is 0; a long key's is a letter byte), so dd_same never merges long keys.  Long keys
+// CAN repeat: k_long_agg emits a partition's keys into the record log once per map call, and a key
+// may also be counted through the long-key table (fallbacks, imports).  Those repeats share their
+// 16-byte prefix, so they land in one tie group, and the tie kernels (k_tie_tiny / k_tie_sort)
+// merge equal full keys - which only happens because sort_records runs the tie pass whenever
+// nlong + lemit >= 2 (wcg_api.hip): a change to that gate must keep repeated long keys merged.
 __device__ __forceinline__ bool dd_same(u64 ah, u64 al, u64 bh, u64 bl) {
     return ah == bh && al == bl && (al & 0xFFu) == 0;
 }

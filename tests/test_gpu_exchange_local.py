@@ -108,3 +108,29 @@ def test_reduce_twice_and_after_free(built):
         e.partitions(5)                                # partition, then reduce again
         e.reduce()
         ob.assert_same(e.result(), want)
+
+
+def test_exchange_local_full_table_fails_every_context(built):
+    """the status agreement of wcg_exchange, driven through
+    wcg_exchange_local.  One context's table overflows (max_keys far below the keys of its range):
+    the exchange fails on every context with that status, the others' errors name the failed
+    rank, no data moves, and the healthy context still reduces its own range exactly."""
+    import wcg
+    from tests import oracle_bridge as ob
+    data = _corpus(seed=91, size=1 << 20)
+    (a0, b0), (a1, b1) = _ranges(data, 2)
+    engines = [wcg.Engine(device=0, max_keys=1 << 18), wcg.Engine(device=0, max_keys=1 << 7)]
+    try:
+        for e, (a, b) in zip(engines, [(a0, b0), (a1, b1)]):
+            e.reset()
+            e.map_host(data[a:b])
+        with pytest.raises(wcg.WcgError) as ei:
+            wcg.exchange_local(engines, 4)
+        from wcg._lib import WCG_EFULL
+        assert ei.value.status == WCG_EFULL
+        assert "rank 1 failed" in str(ei.value)              # context 0's error names the rank
+        engines[0].reduce()
+        ob.assert_same(engines[0].result(), ob.merged(data[a0:b0]))
+    finally:
+        for e in engines:
+            e.close()

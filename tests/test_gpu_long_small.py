@@ -101,3 +101,23 @@ def test_many_long_tokens_then_few(eng):
     run(eng, big)                                               # hint > 4096: the partitioned kernels
     run(eng, b"few long tokens: abcdefghijklmnopqrstuvwxyz abcdefghijklmnopqrstuvwxyz\n")
     run(eng, big[: len(big) // 3].rsplit(b" ", 1)[0] + b"\n")   # hint 2: small again
+
+
+def test_large_context_jobs_do_not_leak_long_keys(built):
+    """a large context (max_keys > 4M: two-pass aggregation, and wcg_reset clears
+    only the listed table claims) runs jobs with different long-key sets, two map calls each, with
+    a reset between them; every job's output must be its own input's, exactly (a claim missing
+    from the list would leave an earlier job's key behind)."""
+    import wcg
+    rnd = random.Random(11)
+    with wcg.Engine(device=0, max_input_bytes=16 << 20, max_keys=5_000_000) as e:
+        for job in range(3):
+            keys = [f"job{'abc'[job]}longkey" + "".join(rnd.choice("defghijkl") for _ in range(8 + job * 5))
+                    for _ in range(400)]
+            calls = [(" ".join(rnd.choice(keys) for _ in range(3000)) + " " + filler(rnd, 500) + "\n").encode()
+                     for _ in range(2)]
+            e.reset()
+            for c in calls:
+                e.map_host(c)
+            e.reduce()
+            ob.assert_same(e.result(), ob.merged(b"".join(calls)))
