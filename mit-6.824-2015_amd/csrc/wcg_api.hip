@@ -363,14 +363,16 @@ int compact(wcg_ctx* c, bool defer = false) {
 
 // One-launch reduce (wcg_fused.h) of a one-pass job: when the previous job of the context had at
 // most FR_NMAX keys (the plan of the device-sized path, which this replaces for small jobs) and no
-// record log or import is involved.  WCG_FUSED=0 keeps the multi-launch path (A/B, tests).
+// record log is involved.  Imported keys (the owners' reduce after wcg_exchange) are table entries
+// like any others (k_import inserts them exactly; a malformed unit sets bad_input, which the
+// launch reports).  WCG_FUSED=0 keeps the multi-launch path (A/B, tests).
 u64 merged_bound(wcg_ctx* c, u64 n, bool json);
 
 bool fused_eligible(wcg_ctx* c) {
     static const char* env = getenv("WCG_FUSED");
     static const bool exact_env = getenv("WCG_EXACT_REDUCE") != nullptr || getenv("WCG_SORT_TARGET") != nullptr;
     if (env && atoi(env) == 0) return false;
-    return !c->compacted && !c->two_pass_used && !c->imported && !exact_env && c->nrec_hint >= 2 &&
+    return !c->compacted && !c->two_pass_used && !exact_env && c->nrec_hint >= 2 &&
            c->nrec_hint <= FR_NMAX;
 }
 

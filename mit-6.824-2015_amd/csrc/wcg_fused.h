@@ -19,7 +19,9 @@
 //                    wcg_sort.h), long keys sharing a 16-byte prefix ordered by their full bytes,
 //                    the lines staged in LDS and written with 16-byte stores at the bucket's place
 //                    (the exclusive prefix of the byte counts: no bucket waits for another)
-// Work is handed out by per-phase ticket counters, and a workgroup waits for a phase only once
+// Work is handed out by per-phase ticket counters (64 shards per phase: shard s hands out items s,
+// s + 64, ...; a workgroup draws from shard blockIdx % 64 and, once that is empty, from any other
+// that its wave's lanes see open), and a workgroup waits for a phase only once
 // every item of the phase before it has been taken (by running workgroups), so the launch cannot
 // deadlock whatever the residency: a workgroup that starts late finds no tickets and leaves.  The
 // workgroup that completes a phase's last item publishes the next phase's parameters (release
@@ -70,14 +72,15 @@ constexpr u32 FR_SHARDS = 8;             // done counters per phase (workgroup %
 #define FR_ENTRY_ACQUIRE 0      // 1: an agent acquire at every phase entry (measurement only)
 #endif
 constexpr u32 FR_SPREAD = 4096 / sizeof(u32);
+constexpr u32 FR_TSHARDS = 64;           // ticket shards per phase (one lane each in the draw)
 constexpr u32 FR_RCOPIES = 16;           // copies of each ready word; workgroup w polls w % 16
 struct FrCtl {
-    u32 ticket[FR_NPH][32];
     u32 done[FR_NPH][32];                // top: shards completed
     u32 exits[32];
     u32 nspill[32];
     u64 B, pad[7];                       // parameters (plain stores before a ready word)
     u32 dshard[FR_NPH][FR_SHARDS][FR_SPREAD];    // items completed per shard
+    u32 tk[FR_NPH][FR_TSHARDS][FR_SPREAD];       // tickets drawn per shard (may pass its item count)
     u64 ready[FR_NPH][FR_RCOPIES][FR_SPREAD / 2];   // epoch | B << 32 once the phase's parameters are out
 };
 
@@ -759,8 +762,13 @@ __global__ __launch_bounds__(FR_NT, 2) void k_fused_reduce(FrArgs a) {
     if (clk) { clk[0] = wall_clock64(); for (int k = 1; k < FR_CLK; k++) clk[k] = 0; }
     bool failed = false, have_sp = false;
     for (int p = 0; p < FR_NPH && !failed; p++) {
+        u32 pre_t = ~0u;                          // (thread 0) the phase's first ticket, drawn early
         if (p > 0) {
             if (tid == 0) {
+                // the first ticket of the phase is drawn before its ready word is seen (a ticket
+                // is only a number until the phase's item count is known): its round trip overlaps
+                // the wait.  Still no residency assumption: it is drawn by a running workgroup.
+                pre_t = fr_add(&C->tk[p][blockIdx.x % FR_TSHARDS][0], 1u);
                 u32 spins = 0, f = 0;
                 u64 rw;
                 while ((u32)(rw = fr_poll64(&C->ready[p][blockIdx.x % FR_RCOPIES][0])) != g.epoch) {
@@ -782,13 +790,42 @@ __global__ __launch_bounds__(FR_NT, 2) void k_fused_reduce(FrArgs a) {
         bool first_item = true;
         const u64 nitems = p == 0 ? FR_SMAX / FR_SPI : p == 1 ? (B > 1 ? FR_SMAX / FR_SPI : 0) : p == 2 ? g.nitems0 : B;
         for (bool first = true;; first = false) {
-            // the first item of a phase is the workgroup's own number (512 workgroups taking a ticket
-            // from one word at once queued 3-6 us); past the grid, tickets (counted from gridDim.x)
-            if (!first && nitems <= gridDim.x) break;     // (no ticketed items this phase)
-            if (tid == 0 && !first) fr_s_item = gridDim.x + fr_add(&C->ticket[p][0], 1u);
-            if (tid == 0 && first) fr_s_item = blockIdx.x;
+            // A ticket from this workgroup's shard (8 workgroups per word: 512 on one word queued
+            // 3-6 us, 64 on one ~1 us), else from any other shard still open: wave 0's 64 lanes
+            // read the 64 shard counters at once and the first open one is drawn from.  A workgroup leaves the phase
+            // only once it has SEEN every shard empty, so every item has been drawn by a running
+            // workgroup before anyone waits for the next phase: no residency assumption (a fixed
+            // first item per workgroup deadlocked when another process's kernel held half the CUs
+            // and the item's workgroup could not start).
+            if (tid < 64) {
+                const u32 lane = tid, sh = (blockIdx.x + lane) % FR_TSHARDS;
+                const u32 lim = nitems > sh ? (u32)((nitems - sh + FR_TSHARDS - 1) / FR_TSHARDS) : 0u;
+                u32 item = ~0u;
+                if (first) {                      // the phase's first draw: straight at the own shard
+                    u32 got = ~0u;
+                    if (lane == 0) {
+                        const u32 t = p > 0 ? pre_t : fr_add(&C->tk[p][sh][0], 1u);
+                        if (t < lim) got = sh + FR_TSHARDS * t;
+                    }
+                    item = (u32)__shfl((int)got, 0, 64);
+                }
+                while (item == ~0u) {
+                    const u32 v = lim ? fr_poll(&C->tk[p][sh][0]) : 0u;
+                    const u64 open = __ballot(v < lim);
+                    if (!open) break;                                  // every shard drawn out
+                    const u32 pick = (u32)__builtin_ctzll(open);       // own shard first
+                    u32 got = ~0u;
+                    if (lane == pick) {
+                        const u32 t = fr_add(&C->tk[p][sh][0], 1u);
+                        if (t < lim) got = sh + FR_TSHARDS * t;
+                    }
+                    got = (u32)__shfl((int)got, (int)pick, 64);
+                    if (got != ~0u) { item = got; break; }
+                }
+                if (lane == 0) fr_s_item = item;
+            }
             __syncthreads();
-            const u64 item = fr_s_item;
+            const u64 item = fr_s_item == ~0u ? ~0ull : (u64)fr_s_item;
             __syncthreads();
             if (item >= nitems) break;
             if (clk && first_item) clk[2 + 3 * p] = wall_clock64();
@@ -814,8 +851,7 @@ __global__ __launch_bounds__(FR_NT, 2) void k_fused_reduce(FrArgs a) {
             __syncthreads();
             if (ick) ick[6] = wall_clock64();
             if (tid == 0) {
-                // item i counts in shard i % FR_SHARDS (the first round's items are the workgroups'
-                // own numbers, so neighbouring workgroups hit different words)
+                // item i counts in shard i % FR_SHARDS (neighbouring items hit different words)
                 const u32 ish = (u32)(item % FR_SHARDS);
                 const u64 per = nitems / FR_SHARDS + ((u64)ish < nitems % FR_SHARDS ? 1 : 0);
                 u32 last = 0;
@@ -837,8 +873,9 @@ __global__ __launch_bounds__(FR_NT, 2) void k_fused_reduce(FrArgs a) {
     __syncthreads();
     if (tid == 0 && fr_add(&C->exits[0], 1u) == gridDim.x - 1) {
         for (int p = 0; p < FR_NPH; p++) {
-            C->ticket[p][0] = 0; C->done[p][0] = 0;
+            C->done[p][0] = 0;
             for (u32 k = 0; k < FR_SHARDS; k++) C->dshard[p][k][0] = 0;
+            for (u32 k = 0; k < FR_TSHARDS; k++) C->tk[p][k][0] = 0;
         }
         C->nspill[0] = 0;
         C->exits[0] = 0;

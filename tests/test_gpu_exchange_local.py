@@ -42,8 +42,10 @@ def test_exchange_gather_local(built, W, root, nreduce):
                 e.map_host(data[a:b])
             sent, received = wcg.exchange_local(engines, nreduce)
             assert sum(sent) == sum(received)
+            paths = []
             for p, e in enumerate(engines):
                 e.reduce()
+                paths.append(e.reduce_path())
                 if nreduce >= W:
                     parts = e.partitions(nreduce)
                     for r in range(nreduce):
@@ -52,6 +54,9 @@ def test_exchange_gather_local(built, W, root, nreduce):
                         else:
                             assert parts[r] == b"", (p, r)
                     e.reduce()                         # partitions() reordered the records: sort again
+            # the owners' reduce of the second job (imported keys) takes the one-launch reduce
+            # wherever the first job left a key count
+            assert (1 in paths) == (rep == 1), paths
             nk, nb = wcg.gather_merge_local(engines, root)
             assert nk == ref.nkeys and nb == len(want)
             ob.assert_same(engines[root].result(), want)

@@ -204,3 +204,28 @@ def test_async_error_surfaces_at_wait(built):
         assert ex.value.status == WCG_EFULL
         nk, got = job(e, small)
         ob.assert_same(got, ob.merged(small))
+
+
+def test_two_contexts_fused_concurrently(built):
+    """Two contexts' one-launch reduces queued at once on their own streams run side by side on
+    the GPU, so neither launch has all its workgroups resident: work must be handed out without a
+    residency assumption (a fixed first item per workgroup deadlocked when another process's
+    launch held half the CUs: the N = 2 rehearsal on one GPU)."""
+    import wcg
+    engines = [wcg.Engine(device=0, max_input_bytes=64 << 20, max_keys=1 << 18) for _ in range(2)]
+    datas = [corpus(30_000, 300_000, seed=s) for s in (3, 4)]
+    wants = [ob.merged(d) for d in datas]
+    try:
+        for rep in range(4):
+            for e, d in zip(engines, datas):
+                e.reset()
+                e.map_host(d)
+            for e in engines:
+                e.reduce_async()
+            for e, want in zip(engines, wants):
+                e.reduce_wait()
+                ob.assert_same(e.result(), want)
+                assert e.reduce_path() == (1 if rep else 0)
+    finally:
+        for e in engines:
+            e.close()
