@@ -862,16 +862,32 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_hist(SortArgs a) 
 #ifndef WCG_SS_SPLIT
 #define WCG_SS_SPLIT 1
 #endif
-constexpr u32 SS_TOP2 = 8192;
+// r05: the top splitters sit in LDS in Eytzinger (breadth-first) order: node k of
+// a perfect tree of SS_TOP_D levels at top_e[k], k = 1 .. 2^D - 1.  A sorted array searched by
+// bisection sends every lane of a wave to the same few midpoints in its first levels, and those
+// midpoints (multiples of large powers of two) all fall in one LDS bank: 92% of the search's LDS
+// cycles were bank conflicts (r04_pmc_c4_1gib_final.txt).  Breadth-first, the nodes of the first
+// levels are neighbours (different banks), and the descent k -> 2k + (x >= node) ends at leaf
+// 2^D + (the number of top splitters <= x): the same count as the bisection.
+constexpr u32 SS_TOP_D = 13;
+constexpr u32 SS_TOP2 = (1u << SS_TOP_D) - 1;  // top splitters: 8191
 constexpr int SSF_NT = 1024;
 __device__ __forceinline__ u32 ss_ntop2(const SortArgs& a) { return a.B - 1 < SS_TOP2 ? a.B - 1 : SS_TOP2; }
 __device__ __forceinline__ u32 ss_top2_index(const SortArgs& a, u32 t, u32 ntop) {
-    return (t + 1) * (a.B - 1) / (ntop + 1);     // < 8193 * 32767 < 2^32: a 32-bit division
+    return (t + 1) * (a.B - 1) / (ntop + 1);     // < 8192 * 32767 < 2^32: a 32-bit division
+}
+// the sorted position of breadth-first node k
+__device__ __forceinline__ u32 ss_top_inorder(u32 k) {
+    const u32 d = 31u - (u32)__builtin_clz(k), h = SS_TOP_D - 1 - d;
+    return ((((k - (1u << d)) << 1) + 1) << h) - 1;
 }
 __global__ __launch_bounds__(SSF_NT) void k_ss_find(SortArgs a) {
-    __shared__ u64 top_hi[SS_TOP2];
+    __shared__ u64 top_e[SS_TOP2 + 1];
     const u32 ntop = ss_ntop2(a);
-    for (u32 t = threadIdx.x; t < ntop; t += SSF_NT) top_hi[t] = a.sph[ss_top2_index(a, t, ntop)];
+    for (u32 k = threadIdx.x + 1; k <= SS_TOP2; k += SSF_NT) {
+        const u32 t = ss_top_inorder(k);
+        top_e[k] = t < ntop ? a.sph[ss_top2_index(a, t, ntop)] : ~0ull;   // past ntop: above every key
+    }
     __syncthreads();
     const u64 n = ss_count(a);
     const u64 stride = (u64)gridDim.x * SSF_NT;
@@ -888,18 +904,22 @@ __global__ __launch_bounds__(SSF_NT) void k_ss_find(SortArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < SS_U; k++) {
-            u32 tl = 0, th = ntop;                    // top splitters <= x (LDS, hi words)
-            while (tl < th) {
-                const u32 mid = (tl + th) >> 1;
-                const u64 sh = top_hi[mid];
+            u32 e = 1;                                // top splitters <= x (LDS, hi words)
+            for (u32 lev = 0; lev < SS_TOP_D; lev++) {
+                const u64 sh = top_e[e];
                 bool lt;
                 if (hi[k] != sh) lt = hi[k] < sh;
                 else {
-                    const u32 g = ss_top2_index(a, mid, ntop);
-                    lt = key3_lt(hi[k], lo[k], si[k], sh, a.spl[g], a.spi[g]);
+                    const u32 t = ss_top_inorder(e);
+                    if (t >= ntop) lt = true;         // padding (an all-ones prefix meets it)
+                    else {
+                        const u32 g = ss_top2_index(a, t, ntop);
+                        lt = key3_lt(hi[k], lo[k], si[k], sh, a.spl[g], a.spi[g]);
+                    }
                 }
-                if (!lt) tl = mid + 1; else th = mid;
+                e = 2 * e + (lt ? 0u : 1u);
             }
+            const u32 tl = e - (1u << SS_TOP_D);
             l[k] = tl > 0 ? ss_top2_index(a, tl - 1, ntop) + 1 : 0;
             m[k] = (tl < ntop ? ss_top2_index(a, tl, ntop) : a.B - 1) - l[k];
         }
