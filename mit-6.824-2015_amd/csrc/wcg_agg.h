@@ -73,6 +73,8 @@ struct AggArgs {
     Rec* ovf;              // pass 2: per-workgroup staging of the entries a full LDS table
     u32 ovf_cap;           //   cannot take (ovf_cap records per workgroup)
     u64* clk;              // diagnostics (WCG_AGG_CLOCK): per workgroup start / end wall clock, or null
+    uint16_t* flist;       // one-pass flush (r05): the occupied slots of workgroup bi's table at
+                           // flist + bi * AGG_NB * AGG_W (null: the slot-by-slot flush)
 };
 
 // bucket choices of pass 2's tables: the high half of the 64-bit key hash (a sub-bucket's keys
@@ -339,7 +341,36 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
     agg_wait_A<0>(a0, a1, a2);                        // nothing may land in a dead register
     agg_wait_B<0>(b0, b1, b2);
     __syncthreads();
-    if (!emit) {
+    if (!emit && a.flist && !a.spill_cap && WCG_AGG_ABLATE != 3) {
+        // ---- one-pass flush (r05): the occupied slots listed first, then the inserts dealt
+        // evenly.  The slot-by-slot loop ran 6.5 iterations per thread, and in nearly every wave
+        // some lane of each iteration held a key (23% of the slots), so a workgroup paid 6.5
+        // dependent insert chains (~38 us of its ~244: WCG_AGG_ABLATE=3); listed, ~1.5 keys per
+        // thread are 2 chains.  (The list goes through global memory: the LDS is the table.)
+        constexpr u32 NE = AGG_NB * AGG_W;
+        uint16_t* const L = a.flist + (u64)bi * NE;
+        u32 mine = 0;
+        for (int i = tid; i < (int)NE; i += AGG_NT) mine += (&tcnt[0][0])[i] ? 1u : 0u;
+        u32 incl = mine;
+        for (int d = 1; d < 64; d <<= 1) { const u32 y = __shfl_up(incl, d, 64); if (lane >= (u32)d) incl += y; }
+        if (lane == 63) wsum[wave][0] = incl;
+        __syncthreads();
+        u32 pos = 0, all = 0;
+        for (u32 w = 0; w < AGG_NT / 64; w++) { if (w < wave) pos += (u32)wsum[w][0]; all += (u32)wsum[w][0]; }
+        pos += incl - mine;
+        for (int i = tid; i < (int)NE; i += AGG_NT)
+            if ((&tcnt[0][0])[i]) L[pos++] = (uint16_t)i;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (u32 j = tid; j < all; j += AGG_NT) {
+            // (an L1-bypassing read: other waves of this workgroup wrote the list)
+            const u32 i = __hip_atomic_load(&L[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u64 c = (&tcnt[0][0])[i], k0 = (&tk0[0][0])[i], k1 = (&tk1[0][0])[i];
+            my_global++;
+            ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
+        }
+        __syncthreads();
+    } else if (!emit) {
         // one-pass mode: the table goes to the global table (one insert per slice and key);
         // two-pass mode: it is spilled too, so every inline key of the bucket reaches exactly one
         // pass-2 sub-bucket and is emitted once per map call (no duplicate with the global table)

@@ -168,6 +168,7 @@ struct wcg_ctx {
     u32 fr_epoch = 0;
     bool fused_last = false;                  // the last wcg_reduce took that path (diagnostics)
     bool pending = false;                     // wcg_reduce_async queued a job not yet read back
+    uint16_t* flist = nullptr; u64 flist_cap = 0;   // r05: k_agg's one-pass flush lists
     u64* h_st_dev = nullptr;                  // h_st's device address (the fused launch writes it)
     std::string err;
 };
@@ -1097,7 +1098,7 @@ int wcg_close(wcg_ctx* c) {
                     c->d_part, c->owner, c->d_per_rank, c->exp_buf, c->pool, c->region_len, c->wg_stats,
                     c->llog, c->llog_len, c->smp, c->bid, c->spx, c->irec, c->lent, c->lpcur, c->spill, c->spill_len, c->pool2, c->rlen2, c->remit, c->ovf, c->hist, c->spart, c->ikey, c->iidx, c->groups,
                     c->pid, c->d_partb, c->nlpos, c->d_rb, c->d_b0, c->d_jin, c->d_jout, c->jhist, c->dbig,
-                    c->d_xrow, c->xrecv, c->grecv, c->glist, c->llist, c->fr_buf};
+                    c->d_xrow, c->xrecv, c->grecv, c->glist, c->llist, c->fr_buf, c->flist};
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (c->h_x) (void)hipHostFree(c->h_x);
@@ -1480,6 +1481,13 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g.emit = c->remit; g.emit_cap = rec_cap_emit;
     g.ovf = nullptr; g.ovf_cap = 0;
     g.clk = nullptr;
+    // one-pass flush through a list of the occupied slots (WCG_AGG_FLIST = 0: slot by slot)
+    g.flist = nullptr;
+    static const char* fl_env = getenv("WCG_AGG_FLIST");
+    if (!two_pass && !(fl_env && atoi(fl_env) == 0)) {
+        RC(ensure(c, &c->flist, &c->flist_cap, (u64)nb1 * AGG_NB * AGG_W));
+        g.flist = c->flist;
+    }
     static const bool agg_clock = getenv("WCG_AGG_CLOCK") != nullptr;
     static u64* d_clk = nullptr;
     if (agg_clock && !two_pass) {          // diagnostics: per-workgroup time against its units
