@@ -705,9 +705,13 @@ int sort_records(wcg_ctx* c) {
     // enough workgroups that each thread takes a few records (the bucket search is a chain of
     // dependent reads); the large-B kernels keep one 128 KiB histogram per CU
     a.G = (u32)std::max<u64>(1, std::min<u64>(cdiv(np, small ? 1024 : 4096), (u64)c->ncu * (small ? 4 : 1)));
-    RC(ensure(c, &c->bid, &c->bid_cap, n));
     // large B: a workgroup-major histogram and the bucket starts after it (B + 1 entries)
     const bool tr = !small && WCG_SS_TR;
+    // the two-pass scatter: the records' buckets after pass 1 (n) and the cursors (B, and 256
+    // coarse ones SX_CS apart)
+    static const bool sx_off = getenv("WCG_SS_SX_OFF") != nullptr;   // A/B: the one-pass scatter
+    const bool sx = tr && WCG_SS_SX && !sx_off;
+    RC(ensure(c, &c->bid, &c->bid_cap, sx ? 2 * n + a.B + 256 * SX_CS : n));
     RC(ensure(c, &c->hist, &c->hist_cap, (u64)a.B * a.G + (tr ? a.B + 1 : 0)));
     RC(ensure(c, &c->irec, &c->irec_cap, 2 * n));
     a.bid = c->bid; a.hist = c->hist;
@@ -744,8 +748,21 @@ int sort_records(wcg_ctx* c) {
     } else {
         RC(scan_u32(c, c->hist, (u64)a.B * a.G));
     }
-    if (small) k_ss_scatter<true><<<a.G, SS_NT, 0, c->stream>>>(a);
-    else k_ss_scatter<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
+    if (small) {
+        k_ss_scatter<true><<<a.G, SS_NT, 0, c->stream>>>(a);
+    } else if (sx) {                               // coarse buckets, then buckets (wcg_sort.h)
+        const u32 lb = a.B > 1 ? 32u - (u32)__builtin_clz(a.B - 1u) : 0u;   // bits of B - 1
+        const u32 sh = lb > 8 ? lb - 8 : 0;        // <= 256 coarse buckets
+        u32* bid2 = c->bid + n;
+        u32* fcur = bid2 + n;
+        u32* ccur = fcur + a.B;
+        k_ss_sxinit<<<cdiv(a.B, 256), 256, 0, c->stream>>>(a, ccur, fcur, sh);
+        const unsigned tiles = (unsigned)std::max<u64>(1, cdiv(n, SX_T));
+        k_ss_sx<1><<<tiles, SX_NT, 0, c->stream>>>(a, SxArgs{a.rec, a.bid, a.irec2, bid2, ccur, sh});
+        k_ss_sx<2><<<tiles, SX_NT, 0, c->stream>>>(a, SxArgs{a.irec2, bid2, a.irec, nullptr, fcur, sh});
+    } else {
+        k_ss_scatter<false><<<a.G, SSL_NT, 0, c->stream>>>(a);
+    }
     k_ss_bucket<0><<<a.B, SB_NT, 0, c->stream>>>(a);
     k_ss_bucket<1><<<a.B, SB_NT, 0, c->stream>>>(a);
     if (a.cls2) k_ss_bucket<2><<<a.B, SB_NT2, 0, c->stream>>>(a);

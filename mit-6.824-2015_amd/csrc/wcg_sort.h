@@ -1036,6 +1036,153 @@ __global__ __launch_bounds__(SMALL ? SS_NT : SSL_NT) void k_ss_scatter(SortArgs 
     }
 }
 
+// r05: the large-B scatter in two passes.  One pass (k_ss_scatter) put every
+// record straight into its bucket among up to 32768: runs of ~3 records per (workgroup, bucket),
+// so nearly every write was a lone 32-byte piece of a line.  Here pass 1 moves each record into
+// its coarse bucket (bucket >> sh: at most 256, each the final range of 2^sh consecutive
+// buckets) and pass 2, within that range, into its bucket.  A pass takes a tile of SX_T records:
+// their keys ranked in LDS, one global cursor reservation per key present in the tile, then the
+// tile written in key order (runs of SX_T / keys records: 16 in pass 1 at 256 coarse buckets,
+// 32 in pass 2 at 128 buckets per range), every store coalesced with its neighbours.  Pass 2's
+// tiles span one or two coarse ranges; a tile whose buckets span more than SX_NK (tiny ranges)
+// reserves per record, as the one-pass scatter does.  Twice the record traffic of one pass, in
+// whole lines.
+#ifndef WCG_SS_SX
+#define WCG_SS_SX 1
+#endif
+#ifndef WCG_SX_NT
+#define WCG_SX_NT 1024
+#endif
+#ifndef WCG_SX_T
+#define WCG_SX_T 4096
+#endif
+constexpr int SX_NT = WCG_SX_NT;
+constexpr u32 SX_T = WCG_SX_T;             // records per tile (u16 positions in LDS)
+constexpr int SX_R = SX_T / SX_NT;
+constexpr u32 SX_NK = 1024;                // keys ranked in LDS
+constexpr u32 SX_CS = 1024;                // coarse cursors 4 KiB apart: every workgroup of pass 1
+                                           // reserves on all of them (one line each, not eight)
+struct SxArgs {
+    const Rec* in; const u32* bin;         // records and their buckets
+    Rec* out; u32* bout;                   // pass 1 also moves the buckets (bout)
+    u32* cur;                              // pass 1: coarse cursors (SX_CS apart); pass 2: bucket cursors
+    u32 sh;                                // coarse bucket = bucket >> sh
+};
+
+// cursors at the bucket starts: fcur[b] = bstart[b], ccur[c] = bstart[c << sh]
+__global__ void k_ss_sxinit(SortArgs a, u32* ccur, u32* fcur, u32 sh) {
+    const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.B) return;
+    const u32 s = a.bstart[b];
+    fcur[b] = s;
+    if ((b & ((1u << sh) - 1u)) == 0u) ccur[(b >> sh) * SX_CS] = s;
+}
+
+template <int PASS>
+__global__ __launch_bounds__(SX_NT) void k_ss_sx(SortArgs a, SxArgs x) {
+    __shared__ u32 hcnt[SX_NK];            // key counts -> the keys' first positions in the tile
+    __shared__ u32 gb[SX_NK];              // the keys' reserved global positions
+    __shared__ uint16_t perm[SX_T];        // tile record at position p (key order)
+    __shared__ u32 pbk[SX_T];              // its bucket
+    __shared__ u32 wred[2][SX_NT / 64];
+    const u64 n = ss_count(a);
+    const u64 t0 = (u64)blockIdx.x * SX_T;
+    if (t0 >= n) return;                   // workgroup-uniform (device-sized sorts)
+    const u32 m = (u32)(n - t0 < SX_T ? n - t0 : SX_T);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    u32 b[SX_R];
+#pragma unroll
+    for (int k = 0; k < SX_R; k++) {
+        const u32 i = tid + k * SX_NT;
+        b[k] = i < m ? x.bin[t0 + i] : ~0u;
+    }
+    u32 kmin = 0, nk;
+    if (PASS == 1) {
+        nk = ((a.B - 1u) >> x.sh) + 1u;
+    } else {
+        u32 lo = ~0u, hi = 0;
+#pragma unroll
+        for (int k = 0; k < SX_R; k++)
+            if (b[k] != ~0u) { lo = min(lo, b[k]); hi = max(hi, b[k]); }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            lo = min(lo, (u32)__shfl_xor((int)lo, d, 64));
+            hi = max(hi, (u32)__shfl_xor((int)hi, d, 64));
+        }
+        if (lane == 0) { wred[0][w] = lo; wred[1][w] = hi; }
+        __syncthreads();
+        lo = ~0u; hi = 0;
+        for (int k = 0; k < SX_NT / 64; k++) { lo = min(lo, wred[0][k]); hi = max(hi, wred[1][k]); }
+        kmin = lo;
+        nk = hi - lo + 1u;                 // m >= 1: lo <= hi
+        if (nk > SX_NK) {                  // workgroup-uniform: one reservation per record
+#pragma unroll
+            for (int k = 0; k < SX_R; k++) {
+                const u32 i = tid + k * SX_NT;
+                if (i < m) x.out[atomicAdd(&x.cur[b[k]], 1u)] = x.in[t0 + i];
+            }
+            return;
+        }
+    }
+    for (u32 j = tid; j < nk; j += SX_NT) hcnt[j] = 0;
+    __syncthreads();
+    u32 r[SX_R];
+#pragma unroll
+    for (int k = 0; k < SX_R; k++) {
+        const u32 key = PASS == 1 ? b[k] >> x.sh : b[k] - kmin;
+        r[k] = b[k] != ~0u ? atomicAdd(&hcnt[key], 1u) : 0u;
+    }
+    __syncthreads();
+    // exclusive scan of the counts (consecutive keys per thread) and one global reservation per
+    // key present in the tile
+    constexpr int KP = (SX_NK + SX_NT - 1) / SX_NT;
+    u32 cnt[KP], tot = 0;
+#pragma unroll
+    for (int q = 0; q < KP; q++) {
+        const u32 j = tid * KP + q;
+        cnt[q] = j < nk ? hcnt[j] : 0u;
+        tot += cnt[q];
+    }
+    u32 incl = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = (u32)__shfl_up((int)incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) wred[0][w] = incl;
+    __syncthreads();                       // also: every count read before it is overwritten
+    u32 run = incl - tot;
+    for (int k = 0; k < w; k++) run += wred[0][k];
+#pragma unroll
+    for (int q = 0; q < KP; q++) {
+        const u32 j = tid * KP + q;
+        if (j < nk) {
+            hcnt[j] = run;
+            if (cnt[q]) gb[j] = atomicAdd(&x.cur[PASS == 1 ? j * SX_CS : kmin + j], cnt[q]);
+            run += cnt[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SX_R; k++) {
+        if (b[k] == ~0u) continue;
+        const u32 key = PASS == 1 ? b[k] >> x.sh : b[k] - kmin;
+        const u32 p = hcnt[key] + r[k];
+        perm[p] = (uint16_t)(tid + k * SX_NT);
+        pbk[p] = b[k];
+    }
+    __syncthreads();
+    // the tile in key order, a record per lane pair (16 bytes each): the stores are whole runs,
+    // each load one 32-byte record
+    for (u32 h = tid; h < 2 * m; h += SX_NT) {
+        const u32 p = h >> 1, half = h & 1u;
+        const u32 i = perm[p], bk = pbk[p], kk = PASS == 1 ? bk >> x.sh : bk - kmin;
+        const u32 d = gb[kk] + (p - hcnt[kk]);
+        reinterpret_cast<uint4*>(x.out + d)[half] = reinterpret_cast<const uint4*>(x.in + t0 + i)[half];
+        if (PASS == 1 && half == 0u) x.bout[d] = bk;
+    }
+}
+
 // Workgroup-major histogram (large B): per bucket b, the exclusive prefix over workgroups in place
 // and the bucket's total in bstart[b] (then scanned into the starts).  Threads take consecutive
 // buckets, so every read and write is coalesced.  ([B][G] written by the histogram kernel was a

@@ -63,6 +63,29 @@ def test_sample_sort_bucket_paths(eng, target):
             os.environ["WCG_SORT_TARGET"] = old
 
 
+@pytest.mark.parametrize("nkeys,target", [(60_000, "1"), (150_000, "8"), (400_000, "16")])
+def test_two_pass_scatter(built, nkeys, target):
+    """The large-B scatter's two passes (coarse buckets, then buckets; wcg_sort.h k_ss_sx): ~2
+    records per bucket over 32768 buckets, so pass 2's tiles of 4096 records span more than 1024
+    buckets (the per-record reservation path); 8 per bucket (tiles spanning ~4 coarse ranges,
+    ranked); 16 per bucket over 400k keys.  A fresh
+    context each: its first job takes the sample sort whatever its key count (the one-launch
+    reduce needs a previous job's count)."""
+    import wcg
+    data = _vocab_text(random.Random(nkeys), nkeys)
+    old = os.environ.get("WCG_SORT_TARGET")
+    try:
+        os.environ["WCG_SORT_TARGET"] = target
+        with wcg.Engine(device=0, max_input_bytes=0, max_keys=1 << 21) as e:
+            ob.assert_same(gpu_wc(e, data), ob.merged(data))
+            assert e.reduce_path() != 1
+    finally:
+        if old is None:
+            os.environ.pop("WCG_SORT_TARGET", None)
+        else:
+            os.environ["WCG_SORT_TARGET"] = old
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 100, 4095, 4096, 4097, 20_000])
 def test_sort_small_counts(eng, n):
     rng = random.Random(n)
