@@ -385,27 +385,22 @@ int reduce_fused(wcg_ctx* c) {
     if (!c->fr_buf) {
         // one allocation: regions | spill records | spill buckets | samples and splitters | sample
         // occupancy | counts | bytes | starts | offsets | control block (zeroed once; each launch's
-        // last workgroup re-zeroes its counters)
-        auto al = [](u64 x) { return (x + 255) & ~255ull; };
-        const u64 sz_reg = (u64)FR_BMAX * FR_RCAP * sizeof(Rec), sz_sp = al(total * sizeof(Rec)),
-                  sz_sb = al(total * sizeof(u32)), sz_smp = 4ull * FR_SMAX * sizeof(u64),
-                  sz_occ = al(FR_SMAX * sizeof(u32)), sz_cnt = al(FR_BMAX * sizeof(u32)),
-                  sz_by = al(FR_BMAX * sizeof(u64)), sz_bs = al((FR_BMAX + 1) * sizeof(u64)),
-                  sz_ctl = al(sizeof(FrCtl));
-        const u64 all = sz_reg + sz_sp + sz_sb + sz_smp + sz_occ + sz_cnt + sz_by + 2 * sz_bs + sz_ctl;
-        HIPCHK(c, hipMalloc(&c->fr_buf, all));
-        HIPCHK(c, hipMemsetAsync(c->fr_buf, 0, all, c->stream));
+        // last workgroup re-zeroes its counters); every array on 128-byte lines of its own
+        // (fr_layout, checked at compile time in wcg_fused.h)
+        const FrLayout L = fr_layout(total);
+        HIPCHK(c, hipMalloc(&c->fr_buf, L.all));
+        HIPCHK(c, hipMemsetAsync(c->fr_buf, 0, L.all, c->stream));
         uint8_t* q = c->fr_buf;
-        c->fr.reg = reinterpret_cast<Rec*>(q); q += sz_reg;
-        c->fr.spill = reinterpret_cast<Rec*>(q); q += sz_sp;
-        c->fr.spill_bid = reinterpret_cast<u32*>(q); q += sz_sb;
-        c->fr.smp = reinterpret_cast<u64*>(q); q += sz_smp;
-        c->fr.socc = reinterpret_cast<u32*>(q); q += sz_occ;
-        c->fr.bcnt = reinterpret_cast<u32*>(q); q += sz_cnt;
-        c->fr.bbytes = reinterpret_cast<u64*>(q); q += sz_by;
-        c->fr.bstart = reinterpret_cast<u64*>(q); q += sz_bs;
-        c->fr.boff = reinterpret_cast<u64*>(q); q += sz_bs;
-        c->fr.ctl = reinterpret_cast<FrCtl*>(q);
+        c->fr.reg = reinterpret_cast<Rec*>(q + L.reg);
+        c->fr.spill = reinterpret_cast<Rec*>(q + L.spill);
+        c->fr.spill_bid = reinterpret_cast<u32*>(q + L.spill_bid);
+        c->fr.smp = reinterpret_cast<u64*>(q + L.smp);
+        c->fr.socc = reinterpret_cast<u32*>(q + L.socc);
+        c->fr.bcnt = reinterpret_cast<u32*>(q + L.bcnt);
+        c->fr.bbytes = reinterpret_cast<u64*>(q + L.bbytes);
+        c->fr.bstart = reinterpret_cast<u64*>(q + L.bstart);
+        c->fr.boff = reinterpret_cast<u64*>(q + L.boff);
+        c->fr.ctl = reinterpret_cast<FrCtl*>(q + L.ctl);
         c->fr.spill_cap = total;
     }
     // compaction counts into nrec / nlong: zero after wcg_reset and after a one-pass k_agg

@@ -43,6 +43,8 @@
 // by the workgroup in global memory with the full-key order; a long-key tie run of any length is
 // ordered by counting ranks under the full-key order.
 #pragma once
+#include <cstddef>
+
 #include "wcg_common.h"
 #include "wcg_sort.h"
 #include "wcg_reduce.h"
@@ -78,11 +80,58 @@ struct FrCtl {
     u32 done[FR_NPH][32];                // top: shards completed
     u32 exits[32];
     u32 nspill[32];
-    u64 B, pad[7];                       // parameters (plain stores before a ready word)
+    u64 B, pad[15];                      // parameters (plain stores before a ready word), a line alone
     u32 dshard[FR_NPH][FR_SHARDS][FR_SPREAD];    // items completed per shard
     u32 tk[FR_NPH][FR_TSHARDS][FR_SPREAD];       // tickets drawn per shard (may pass its item count)
     u64 ready[FR_NPH][FR_RCOPIES][FR_SPREAD / 2];   // epoch | B << 32 once the phase's parameters are out
 };
+
+// ---- the hand-over invariant of the header, executable.  Consumers read
+// handed-over data with plain loads and no acquire, which is only exact while no 128-byte line a
+// phase hands over shares a cache line with anything read (or written) before the hand-over.  So:
+// every field of FrCtl that one party writes and another reads starts a line of its own, and every
+// array of the fused reduce's allocation (fr_layout below: bucket regions, spill records, spill
+// buckets, samples and splitters, sample occupancy, counts, bytes, starts, offsets, the control
+// block) starts on a line boundary and ends on one.
+constexpr u64 FR_LINE = 128;
+static_assert(offsetof(FrCtl, done) % FR_LINE == 0 && sizeof(FrCtl::done[0]) == FR_LINE, "done: a line per phase");
+static_assert(offsetof(FrCtl, exits) % FR_LINE == 0 && sizeof(FrCtl::exits) == FR_LINE, "exits: one line");
+static_assert(offsetof(FrCtl, nspill) % FR_LINE == 0 && sizeof(FrCtl::nspill) == FR_LINE, "nspill: one line");
+static_assert(offsetof(FrCtl, B) % FR_LINE == 0 && offsetof(FrCtl, dshard) - offsetof(FrCtl, B) == FR_LINE,
+              "B: a line of its own (it shared one with dshard until r06)");
+static_assert(offsetof(FrCtl, dshard) % FR_LINE == 0 && (FR_SPREAD * sizeof(u32)) % FR_LINE == 0, "dshard: line strides");
+static_assert(offsetof(FrCtl, tk) % FR_LINE == 0, "tk: line strides");
+static_assert(offsetof(FrCtl, ready) % FR_LINE == 0 && (FR_SPREAD / 2 * sizeof(u64)) % FR_LINE == 0, "ready: line strides");
+static_assert(sizeof(FrCtl) % FR_LINE == 0, "the control block ends on a line");
+
+// the allocation's arrays, in order (host: reduce_fused); T = table slots (gtab + ltab)
+struct FrLayout { u64 reg, spill, spill_bid, smp, socc, bcnt, bbytes, bstart, boff, ctl, all; };
+__host__ __device__ constexpr u64 fr_round(u64 x) { return (x + 255) & ~255ull; }
+__host__ __device__ constexpr FrLayout fr_layout(u64 T) {
+    FrLayout L{};
+    u64 q = 0;
+    L.reg = q;       q += fr_round((u64)FR_BMAX * FR_RCAP * sizeof(Rec));
+    L.spill = q;     q += fr_round(T * sizeof(Rec));
+    L.spill_bid = q; q += fr_round(T * sizeof(u32));
+    L.smp = q;       q += fr_round(4ull * FR_SMAX * sizeof(u64));
+    L.socc = q;      q += fr_round(FR_SMAX * sizeof(u32));
+    L.bcnt = q;      q += fr_round(FR_BMAX * sizeof(u32));
+    L.bbytes = q;    q += fr_round(FR_BMAX * sizeof(u64));
+    L.bstart = q;    q += fr_round((FR_BMAX + 1) * sizeof(u64));
+    L.boff = q;      q += fr_round((FR_BMAX + 1) * sizeof(u64));
+    L.ctl = q;       q += fr_round(sizeof(FrCtl));
+    L.all = q;
+    return L;
+}
+__host__ __device__ constexpr bool fr_layout_lines(u64 T) {
+    const FrLayout L = fr_layout(T);
+    const u64 o[] = {L.reg, L.spill, L.spill_bid, L.smp, L.socc, L.bcnt, L.bbytes, L.bstart, L.boff, L.ctl, L.all};
+    for (u64 x : o)
+        if (x % FR_LINE) return false;
+    return true;
+}
+static_assert(fr_layout_lines(1) && fr_layout_lines(3) && fr_layout_lines(1ull << 17) && fr_layout_lines((1ull << 17) + 7) &&
+              fr_layout_lines(12345679), "every fused-reduce array starts and ends on a 128-byte line");
 
 struct FrArgs {
     const GEntry* gtab; u64 gslots;

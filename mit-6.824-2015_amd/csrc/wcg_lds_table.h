@@ -18,6 +18,9 @@
 #ifndef WCG_DIAG_SLOTS
 #define WCG_DIAG_SLOTS 0
 #endif
+#ifndef WCG_DIAG_NOCOUNT
+#define WCG_DIAG_NOCOUNT 0                   // diagnostics: 1 = k_map's short-key hits not counted
+#endif
 
 namespace wcg {
 
@@ -200,14 +203,16 @@ struct MapTable {
         const u32 bit = 1u << (b & 31);
         return (atomicOr(&seen[b >> 5], bit) & bit) != 0;
     }
-    // slot choices from 16-bit fields of h by full-rate 24-bit multiplies (bits 16-31 and
-    // 6-21; bits 0-5 are the miss bucket, so a bucket's keys still spread over both choices)
+    // slot choices from 24-bit fields of h by the high half of full-rate 24-bit multiplies
+    // (v_mul_hi_u32_u24: bits 8-31 and 0-23, each choice ruled by its field's top bits; bits 0-5
+    // are the miss bucket, so a bucket's keys still spread over both choices).  r06: one
+    // instruction per choice (two: the shift) against three (multiply, shift, field extract)
     __device__ __forceinline__ static void slots(u32 h, u32 n, u32& s1, u32& s2) {
 #if WCG_DIAG_SLOTS                           // diagnostics only: conflict-free probes, wrong counts
         s1 = __lane_id(); s2 = __lane_id() + 64; (void)h; (void)n;
 #else
-        s1 = __umul24(h >> 16, n) >> 16;
-        s2 = __umul24((h >> 6) & 0xFFFFu, n) >> 16;
+        s1 = (u32)(((u64)(h >> 8) * (u64)(n << 8)) >> 32);
+        s2 = (u32)(((u64)(h & 0xFFFFFFu) * (u64)(n << 8)) >> 32);
 #endif
     }
     // A probe split in two so that k_map can issue its reads together with the next token's:
@@ -217,7 +222,7 @@ struct MapTable {
     // count add); the insert path (a probe saw an empty slot) is rare once the table has filled.
     struct Probe { u32 s1, s2; u64 x1, x2, y1, y2; };
     __device__ __forceinline__ Probe probe(bool med, u32 h) const {
-        static_assert(NS < 65536 && NM < 65536, "24-bit slot multiply");
+        static_assert(NS < 65536 && NM < 65536, "n << 8 fits the 24-bit multiply");
         Probe p;
         slots(h, med ? (u32)NM : (u32)NS, p.s1, p.s2);
         const u64* K0 = med ? mk0 : sk0;
@@ -239,7 +244,7 @@ struct MapTable {
     }
     __device__ __forceinline__ bool finish_short(u64 a0, u32 h, const ProbeS& p) {
         const bool h1 = p.x1 == a0, hit = h1 || p.x2 == a0;
-        atomicAdd(&scnt[h1 ? p.s1 : p.s2], hit ? 1u : 0u);
+        if (!WCG_DIAG_NOCOUNT) atomicAdd(&scnt[h1 ? p.s1 : p.s2], hit ? 1u : 0u);
         if (hit || (p.x1 != 0 && p.x2 != 0) || !admit(h)) return hit;
         if (p.x1 == 0) {
             const u64 old = atomicCAS(&sk0[p.s1], 0ull, a0);

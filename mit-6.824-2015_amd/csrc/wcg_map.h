@@ -25,10 +25,10 @@
 //
 // Prefetch accounting.  `s_waitcnt vmcnt(N)` waits until all but this wave's N youngest vector
 // memory operations are done (loads and stores retire in issue order).  A step's processing
-// issues exactly 1 miss-log store per short-key iteration and 2 per general iteration, plus 2
-// after its last one (inline-asm buffer stores executed by the whole wave, out-of-range offsets
-// for lanes without a miss), so when set s is due the number of operations issued after its
-// loads is known: the other sets' MAP_SETS - 1 loads + the stores of each of the MAP_SETS - 1
+// issues exactly 1 miss-log store per short-key iteration and 2 per medium-key iteration, plus 2
+// after its last medium iteration (inline-asm buffer stores executed by the whole wave,
+// out-of-range offsets for lanes without a miss), so when set s is due the number of operations
+// issued after its loads is known: the other sets' MAP_SETS - 1 loads + the stores of each of the MAP_SETS - 1
 // steps processed since.  The
 // wait uses the largest quantised N not above that count; any operation the count does not know about (rare paths: long tokens, a full miss-log
 // region, UTF-8 table loads) can only make the wait stronger.
@@ -56,9 +56,6 @@ constexpr int MAP_WREG = MAP_WIN + 8;        // staging (+8: keyread's third wor
 constexpr int MAP_SST = 512;                 // max token starts per step (992 / 2 = 496)
 #ifndef WCG_DIRECT
 #define WCG_DIRECT 0                         // 1: no start list (measured slower: r03_kmap_experiments)
-#endif
-#ifndef WCG_KEYREAD4
-#define WCG_KEYREAD4 1                       // key bytes by dword reads from rp & ~3 (0: b64 pairs)
 #endif
 #ifndef WCG_ADMIT2
 #define WCG_ADMIT2 1                         // k_map LDS tables admit keys on their second miss
@@ -887,7 +884,11 @@ static_assert(MAP_SETS == 2 || MAP_SETS == 4, "k_map's main loop names two or fo
 
 // one miss-log unit store issued by the whole wave (lanes without a unit pass an out-of-range
 // offset: the buffer range check drops the write); counted by the prefetch accounting
+#ifndef WCG_DIAG_NOSTORE
+#define WCG_DIAG_NOSTORE 0                   // diagnostics: 1 = no miss-log stores (wrong counts)
+#endif
 __device__ __forceinline__ void unit_store(v4i rsrc, u32 off, u64 v) {
+    if (WCG_DIAG_NOSTORE) { asm volatile("; wcg-nostore" :: "v"(v), "v"(off), "s"(rsrc) : "memory"); return; }
     asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen ; wcg-store" :: "v"(v), "v"(off), "s"(rsrc) : "memory");
 }
 constexpr u32 OOB = 0xFFFFFFF0u;
@@ -1006,7 +1007,13 @@ __device__ __forceinline__ u32 utf8_mask_list(uint4 c, u32 nx, LdsLetters lt, co
 }
 
 template <int ABL>
-__global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs a) {
+#if WCG_MAP_WGS > 1
+// occupancy experiments (r06): 8 waves per SIMD also needs <= 80 SGPRs
+#define WCG_MAP_ATTR __attribute__((amdgpu_waves_per_eu(4 * WCG_MAP_WGS * WCG_MAP_NT / 1024, 4 * WCG_MAP_WGS * WCG_MAP_NT / 1024)))
+#else
+#define WCG_MAP_ATTR
+#endif
+__global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) WCG_MAP_ATTR void k_map(MapArgs a) {
 #if !WCG_DIRECT
     __shared__ __align__(16) uint8_t wbytes[MAP_WAVES][MAP_WREG];
     __shared__ __align__(16) uint16_t wstart[MAP_WAVES][MAP_SST];
@@ -1053,6 +1060,7 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
     // token starts are owned by lanes 1-62 only (lane 0: the prefix chunk, 63: the look-ahead)
     const u32 own16 = (u32)(lane - 1) < (u32)MAP_OWN ? 0xFFFFu : 0u;
     u32 my_hits = 0, my_global = 0, my_long = 0;
+    u64 hits_w = 0;                              // wave-uniform: hits counted from the hit masks (SALU)
 
     // miss-log stores of this workgroup: one buffer resource over its regions
     const u32 P = a.pmask + 1;
@@ -1074,54 +1082,99 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
     };
 
 #if !WCG_DIRECT
-    // ---- token decoding.  An entry of the start list -> the key's 16 bytes from three aligned
-    //      8-byte LDS reads (unaligned 8-byte LDS reads cost ~20x the LDS cycles), then the key
-    //      identity of fact F4 with byte masks, and its LDS hash
-    struct Tok { u32 e, k0l, k0h, k1l, k1h, h; bool shrt, lng, valid; };
-#if WCG_KEYREAD4
-    // r03: the key's dwords from rp & ~3 (dword reads: ds_read2_b32 pairs), so the word at rp is
-    // one alignbyte away; 8-byte-aligned pairs needed a select of every dword by rp & 4
-    struct KeyWords { u32 d0, d1, d2, d3, d4; };
-    auto keyread = [&](u32 e) -> KeyWords {
-        const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1);
-        const u32* q = reinterpret_cast<const u32*>(bytes + (rp & ~3u));
-        return KeyWords{q[0], q[1], q[2], q[3], q[4]};
+    // ---- token decoding.  An entry of the start list -> the key's bytes from aligned dword LDS
+    //      reads (r03: dwords from rp & ~3, ds_read2_b32 pairs, so the word at rp is one alignbyte
+    //      away; unaligned 8-byte LDS reads cost ~20x the LDS cycles), then the key identity of
+    //      fact F4 with byte masks, and its LDS hash
+    struct TokS { u64 k; u32 h; };                   // short key (<= 7 bytes): k0 alone
+    struct TokM { u64 k0, k1; u32 h; bool valid; };  // medium key (8-15 bytes); long tokens: !valid
+    // short key: its bytes lie in [rp & ~3, +12)
+    auto keyread_s = [&](u32 e) -> uint3 {
+        const u32* q = reinterpret_cast<const u32*>(bytes + ((e & ((1u << SST_LEN_SHIFT) - 1)) & ~3u));
+        return make_uint3(q[0], q[1], q[2]);
     };
-#else
-    struct KeyWords { uint2 q0, q1, q2; };
-    auto keyread = [&](u32 e) -> KeyWords {
-        const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1);
-        const uint2* q = reinterpret_cast<const uint2*>(bytes + (rp & ~7u));
-        return KeyWords{q[0], q[1], q[2]};
-    };
-#endif
-    auto decode_tok = [&](u32 e, bool act, const KeyWords& kw) -> Tok {
-        Tok t;
-        t.e = e;
+    auto decode_s = [&](u32 e, const uint3& kw) -> TokS {
         const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1), len = e >> SST_LEN_SHIFT;
         const u32 bsh = rp & 3u;
-#if WCG_KEYREAD4
-        const u32 e0 = kw.d0, e1 = kw.d1, e2 = kw.d2, e3 = kw.d3, e4 = kw.d4;
-#else
-        const bool hi4 = (rp & 4u) != 0;
-        const u32 e0 = hi4 ? kw.q0.y : kw.q0.x, e1 = hi4 ? kw.q1.x : kw.q0.y, e2 = hi4 ? kw.q1.y : kw.q1.x;
-        const u32 e3 = hi4 ? kw.q2.x : kw.q1.y, e4 = hi4 ? kw.q2.y : kw.q2.x;
-#endif
-        const u32 w0 = __builtin_amdgcn_alignbyte(e1, e0, bsh), w1 = __builtin_amdgcn_alignbyte(e2, e1, bsh);
-        const u32 w2 = __builtin_amdgcn_alignbyte(e3, e2, bsh), w3 = __builtin_amdgcn_alignbyte(e4, e3, bsh);
-        // keep the key's bytes: nb = bytes in the last (partial) word pair, 0..7
-        t.shrt = len < 8;
-        const u32 nb = t.shrt ? len : len - 8;
-        const u32 ml = nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1;
-        const u32 mh = nb >= 4 ? (1u << (8 * nb - 32)) - 1 : 0u;
-        const u32 pl = (t.shrt ? w0 : w2) & ml;
-        const u32 ph = ((t.shrt ? w1 : w3) & mh) | (len << 24);
-        t.k0l = t.shrt ? pl : w0; t.k0h = t.shrt ? ph : w1;
-        t.k1l = t.shrt ? 0u : pl; t.k1h = t.shrt ? 0u : ph;
-        t.lng = act && len >= 16;
-        t.valid = act && len < 16;
-        t.h = lds_hash32(t.k0l, t.k0h, t.k1l, t.k1h);
+        const u64 w = (u64)__builtin_amdgcn_alignbyte(kw.z, kw.y, bsh) << 32 | __builtin_amdgcn_alignbyte(kw.y, kw.x, bsh);
+        TokS t;
+        t.k = (w & ((1ull << (8 * len)) - 1)) | (u64)len << 56;
+        t.h = lds_hash32((u32)t.k, (u32)(t.k >> 32), 0u, 0u);
         return t;
+    };
+    // medium key (or a long token's first 16 bytes): [rp & ~3, +20)
+    struct KeyWords { u32 d0, d1, d2, d3, d4; };
+    auto keyread = [&](u32 e) -> KeyWords {
+        const u32* q = reinterpret_cast<const u32*>(bytes + ((e & ((1u << SST_LEN_SHIFT) - 1)) & ~3u));
+        return KeyWords{q[0], q[1], q[2], q[3], q[4]};
+    };
+    // act: the entry is one of this step's tokens.  A long token (> 15 bytes) is measured and
+    // logged here, while its step's window masks are in LDS (its TokM may be carried to the next
+    // step), and takes no part in the table
+    auto decode_m = [&](u32 e, bool act, const KeyWords& kw, long wbase) -> TokM {
+        const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1), len = e >> SST_LEN_SHIFT;
+        const u32 bsh = rp & 3u;
+        const u32 w0 = __builtin_amdgcn_alignbyte(kw.d1, kw.d0, bsh), w1 = __builtin_amdgcn_alignbyte(kw.d2, kw.d1, bsh);
+        const u32 w2 = __builtin_amdgcn_alignbyte(kw.d3, kw.d2, bsh), w3 = __builtin_amdgcn_alignbyte(kw.d4, kw.d3, bsh);
+        const u32 nb = len - 8;                            // bytes in k1: 0..7
+        const u32 ml = nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1;
+        const u32 mh = nb >= 4 ? (1u << ((8 * nb - 32) & 31)) - 1 : 0u;
+        TokM t;
+        const u32 k1l = w2 & ml, k1h = (w3 & mh) | (len << 24);
+        t.k0 = (u64)w1 << 32 | w0;
+        t.k1 = (u64)k1h << 32 | k1l;
+        t.h = lds_hash32(w0, w1, k1l, k1h);
+        t.valid = act && len < 16;
+        if (act && len >= 16) {
+            my_long++;
+            if (ABL != 6) long_token_log<ABL>(a, (u64)(wbase + rp), rp, wmask[wave], &lcur);
+        }
+        return t;
+    };
+
+    // ---- carried tokens (r06).  A list's last, partial iteration is not run in its step: its
+    //      tokens, already decoded, stay in registers (lanes [0, n)) and fill the first lanes of
+    //      the next step's first iteration, whose list reads are shifted by n (entry i of a step's
+    //      list goes to lane (n + i) % 64).  So every iteration but the wave's last two (the drain
+    //      after the main loop) runs 64 tokens, and short keys never take the medium-key body (C2:
+    //      2 short + 1 mixed iteration per step before, ~2.3 short + ~0.3 medium now)
+    TokS cs{0, 0};
+    TokM cm{0, 0, 0, false};
+    u32 ncs = 0, ncm = 0;                 // carried short / medium tokens (wave-uniform)
+    // A miss reserves its units with an LDS atomic whose result is read one iteration later (after
+    // that iteration's probe reads have returned, so the reservation adds no round trip of its
+    // own), and the wave stores them then: 1 unit store per short iteration, 2 per medium
+    // iteration, 2 after a step's last medium iteration (prefetch accounting); a short miss may
+    // stay pending across steps
+    bool missp = false;                   // the pending miss: bucket, units, reservation and key
+    u32 pp = 0, nup = 0, posp = 0;
+    u64 k0p = 0, k1p = 0;
+    const u32 rcap = (u32)a.region_cap;   // < 2^22 (host), so offsets fit 24-bit multiplies
+    auto store_pending = [&](bool two) {
+        const bool fits = missp && posp + nup <= rcap;
+        const u32 o0 = fits ? (__umul24(pp, rcap) + posp) * 8u : OOB;
+        unit_store(prsrc, o0, k0p);
+        if (two) unit_store(prsrc, fits && nup == 2 ? o0 + 8u : OOB, k1p);
+        if (missp && !fits) {             // region full: zero its tail, global table
+            u64* r = wpool + (u64)pp * a.region_cap;
+            for (u32 k = posp; k < rcap; k++) r[k] = 0;
+            my_global++;
+            ginsert(a.gtab, a.gmask, k0p, k1p, gslot(key_hash(k0p, k1p)), 1, a.st);
+        }
+    };
+    auto miss_short = [&](bool miss, const TokS& t) {
+        missp = miss;
+        pp = miss_bucket(t.h, a.pmask);
+        nup = 1u;
+        posp = atomicAdd(&cursor[pp], miss ? 1u : 0u);   // every lane (0 = no miss)
+        k0p = t.k; k1p = 0;
+    };
+    auto miss_medium = [&](bool miss, const TokM& t) {
+        missp = miss;
+        pp = miss_bucket(t.h, a.pmask);
+        nup = 2u;
+        posp = atomicAdd(&cursor[pp], miss ? 2u : 0u);
+        k0p = t.k0; k1p = t.k1;
     };
 
     // one step: returns the number of unit stores it issued (prefetch accounting)
@@ -1176,179 +1229,95 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
         const u32 tot_s = tot & 0xFFFFu;
         const u32 total = tot_s + (tot >> 16);
         const u32 excl = incl - packed;
-        u32 o_s = excl & 0xFFFFu, o_o = (excl >> 16) + tot_s;
-        // one loop over all starts (two loops, short and other, ran max(short) + max(other) =
-        // 4.2 + 1.6 iterations per step against max(all) = 4.2)
+        const u32 o_s = excl & 0xFFFFu, o_o = (excl >> 16) + tot_s;
+        // r06: the short starts and the others in two loops of straight-line slots (the k-th
+        // start of a lane goes to its list offset + k, an immediate store offset), each ending
+        // when no lane has a start left.  One loop over all starts picked the list and bumped
+        // two offsets per start: 15 VALU per iteration against 9 here, for max(all) = 4.2
+        // iterations per step against max(short) + max(other) = 4.2 + 1.6 (C2)
         const u32 lbase = 16 * lane;
-        while (starts) {
-            const u32 b = __builtin_ctz(starts);
-            starts &= starts - 1;
-            const u32 run = __builtin_ctz(~(w32 >> b));        // >= 1; 32 - b when the window is all letters
-            const u32 len = run < 16 ? run : 16u;              // 16 = long token (> 15 bytes)
-            const bool sh = len < 8;
-            sst[sh ? o_s : o_o] = (uint16_t)((lbase + b) | (len << SST_LEN_SHIFT));
-            o_s += sh ? 1u : 0u;
-            o_o += sh ? 0u : 1u;
-        }
+        auto list = [&](uint16_t* w, u32 msk, bool shrt) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) {                   // <= 8 starts per 16-byte chunk
+                if (__ballot(msk != 0) == 0) break;
+                if (msk) {
+                    const u32 b = __builtin_ctz(msk);
+                    msk &= msk - 1;
+                    const u32 run = __builtin_ctz(~(w32 >> b));   // >= 1; 32 - b when the window is all letters
+                    const u32 len = shrt ? run : (run < 16 ? run : 16u);   // 16 = long token (> 15 bytes)
+                    w[k] = (uint16_t)((lbase + b) | (len << SST_LEN_SHIFT));
+                }
+            }
+        };
+        list(sst + o_s, starts & ~r8, true);
+        list(sst + o_o, starts & r8, false);
         wave_lds_sync();
         stamp(3);
         my_tokens += total;
+        if (ABL >= 1 && ABL <= 3) return 0;   // (r06: levels 2 and 3 are level 1)
 
-        // ---- tokens: uniform iterations of 64 tokens (every lane runs every iteration; lanes
-        //      past `total` are inactive by flag), software-pipelined so that one LDS round trip
-        //      per iteration carries this token's table probe, the next token's key bytes and
-        //      the entry after that.  A miss reserves its units with an LDS atomic whose result
-        //      is read one iteration later (after that iteration's probe reads have returned, so
-        //      the reservation adds no round trip of its own), and the wave stores the units
-        //      then: 1 unit store per short iteration, 2 per general iteration, 2 after the loop
-        //      (prefetch accounting)
-        u32 sink = 0;
-        bool missp = false;                   // the previous iteration's miss: bucket, units,
-        u32 pp = 0, nup = 0, posp = 0;        // reservation and key
-        u64 k0p = 0, k1p = 0;
-        const u32 rcap = (u32)a.region_cap;   // < 2^22 (host), so offsets fit 24-bit multiplies
-        auto store_pending = [&](bool two) {
-            const bool fits = missp && posp + nup <= rcap;
-            const u32 o0 = fits ? (__umul24(pp, rcap) + posp) * 8u : OOB;
-            unit_store(prsrc, o0, k0p);
-            if (two) unit_store(prsrc, fits && nup == 2 ? o0 + 8u : OOB, k1p);
-            if (missp && !fits) {             // region full: zero its tail, global table
-                u64* r = wpool + (u64)pp * a.region_cap;
-                for (u32 k = posp; k < rcap; k++) r[k] = 0;
-                my_global++;
-                ginsert(a.gtab, a.gmask, k0p, k1p, gslot(key_hash(k0p, k1p)), 1, a.st);
-            }
-        };
-        // full iterations of short entries take the short body; the rest (the partial short
-        // iteration, medium and long keys) the general one
-        const u32 nsh = (ABL == 0 || ABL >= 6) ? (tot_s >> 6) : 0u;
-        const u32 first = nsh * 64;
-        const u32 iters = (total - first + 63) >> 6;
-        // Each loop is software-pipelined on its own; reads and decodes past a loop's last
-        // iteration are unconditional and unused (entries past the list read other LDS words,
-        // key reads stay inside the wave's staging bytes), so no loop-carried state is merged
-        // across loop-exit branches.
-        Tok cur;
-        u32 e_nxt;
-        if (nsh) {
-            // short key (<= 7 bytes): its bytes lie in [rp & ~7, +16): two aligned 8-byte reads
-            auto keyread_s = [&](u32 e) -> uint4 {
-                const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1);
-#if WCG_KEYREAD4
-                const u32* q = reinterpret_cast<const u32*>(bytes + (rp & ~3u));
-                return make_uint4(q[0], q[1], q[2], 0u);
-#else
-                const uint2* q = reinterpret_cast<const uint2*>(bytes + (rp & ~7u));
-                const uint2 x = q[0], y = q[1];
-                return make_uint4(x.x, x.y, y.x, y.y);
-#endif
-            };
-            struct TokS { u64 k; u32 h; };
-            auto decode_s = [&](u32 e, const uint4& kw) -> TokS {
-                const u32 rp = e & ((1u << SST_LEN_SHIFT) - 1), len = e >> SST_LEN_SHIFT;
-                const u32 bsh = rp & 3u;
-#if WCG_KEYREAD4
-                const u32 e0 = kw.x, e1 = kw.y, e2 = kw.z;
-#else
-                const bool hi4 = (rp & 4u) != 0;
-                const u32 e0 = hi4 ? kw.y : kw.x, e1 = hi4 ? kw.z : kw.y, e2 = hi4 ? kw.w : kw.z;
-#endif
-                const u64 w = (u64)__builtin_amdgcn_alignbyte(e2, e1, bsh) << 32 | __builtin_amdgcn_alignbyte(e1, e0, bsh);
-                TokS t;
-                t.k = (w & ((1ull << (8 * len)) - 1)) | (u64)len << 56;
-                t.h = lds_hash32((u32)t.k, (u32)(t.k >> 32), 0u, 0u);
-                return t;
-            };
-            u32 it = 0;
-            TokS cs = decode_s(sst[it * 64 + lane], keyread_s(sst[it * 64 + lane]));
-            e_nxt = sst[(it + 1) * 64 + lane];
-            for (; it + 1 < nsh; it++) {
-                const auto pr = tab.probe_short(cs.h);
-                const uint4 nks = keyread_s(e_nxt);
-                const u32 e_nn = sst[(it + 2) * 64 + lane];
-                __builtin_amdgcn_sched_barrier(0);  // all three reads issue before the probe's wait
-                const bool hit = tab.finish_short(cs.k, cs.h, pr);
-                my_hits += (u32)hit;
-                store_pending(false);         // short keys: one unit
-                missp = !hit;
-                pp = miss_bucket(cs.h, a.pmask);
-                nup = 1u;
-                posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
-                k0p = cs.k; k1p = 0;
-                cs = decode_s(e_nxt, nks);
-                e_nxt = e_nn;
-            }
-            // the last short iteration decodes the general loop's first token (entry first +
-            // lane, already in e_nxt) with the general decoder: no prologue round trips there
-            {
-                const auto pr = tab.probe_short(cs.h);
-                const KeyWords nkw = keyread(e_nxt);
-                const u32 e_nn = sst[(it + 2) * 64 + lane];
-                __builtin_amdgcn_sched_barrier(0);
-                const bool hit = tab.finish_short(cs.k, cs.h, pr);
-                my_hits += (u32)hit;
-                store_pending(false);
-                missp = !hit;
-                pp = miss_bucket(cs.h, a.pmask);
-                nup = 1u;
-                posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
-                k0p = cs.k; k1p = 0;
-                cur = decode_tok(e_nxt, first + lane < total, nkw);
-                e_nxt = e_nn;
-            }
-        } else {
-            e_nxt = sst[lane];
-            if (iters) {
-                cur = decode_tok(e_nxt, first + lane < total, keyread(e_nxt));
-                e_nxt = sst[first + 64 + lane];
-            }
+        // ---- tokens: uniform iterations of 64 tokens, the short list first, then the medium/long
+        //      one, each software-pipelined so that one LDS round trip per iteration carries this
+        //      token's table probe, the next token's key bytes and the entry after that; decodes
+        //      past a list's end are unconditional (entries read other LDS words, key reads stay
+        //      inside the wave's staging bytes) and only the carried lanes' ones are used
+        const u32 ts = tot_s, tm = tot >> 16;
+        const u32 ns = ncs + ts, nfs = ns >> 6;          // short tokens; full iterations
+        const u32 nm = ncm + tm, nfm = nm >> 6;          // medium/long tokens; full iterations
+        const u32 ls = (u32)lane - ncs;                  // iteration 0's short entry (wraps for carried lanes)
+        const u32 lm = (u32)lane - ncm;
+        // entry i of an iteration's lane: ps[64 * i] / pm[64 * i] (the carried lanes of iteration
+        // 0 and the lanes past a list's end read other LDS words of the workgroup: unused)
+        const uint16_t* const ps = sst + (int)ls;
+        const uint16_t* const pm = sst + (int)(ts + lm);
+        // both lists' first entries and key bytes in one round trip each
+        const u32 es0 = ps[0], em0 = pm[0];
+        u32 e_nxt = ps[64], f_nxt = pm[64];
+        {
+            const uint3 kws = keyread_s(es0);
+            const KeyWords kwm = keyread(em0);
+            const TokS t = decode_s(es0, kws);
+            const TokM u = decode_m(em0, lm < tm, kwm, wbase);
+            if ((u32)lane >= ncs) cs = t;
+            if ((u32)lane >= ncm) cm = u;
         }
         stamp(4);
-        for (u32 it = 0; it < iters; it++) {
-            const u32 base = first + it * 64;
-            if (ABL == 1) { sink += cur.e; cur.e = sst[base + 64 + lane]; continue; }
-            if (cur.lng) {
-                my_long++;
-                const u32 rp = cur.e & ((1u << SST_LEN_SHIFT) - 1);
-                if (ABL != 6) long_token_log<ABL>(a, (u64)(wbase + rp), rp, wmask[wave], &lcur);
-            }
-            const bool med = !cur.shrt;
-            const u64 k0 = (u64)cur.k0h << 32 | cur.k0l, k1 = (u64)cur.k1h << 32 | cur.k1l;
-            if (ABL == 2) { sink += cur.h; cur = decode_tok(e_nxt, base + 64 + lane < total, keyread(e_nxt));
-                            e_nxt = sst[base + 128 + lane]; continue; }
-            // issue together: this token's probe, the next token's key bytes, the entry after
-            // (none of it in the last iteration: C2 steps run one general iteration, so its
-            // next-token reads and decode were pure waste, ~40 VALU per step)
-            const bool more = it + 1 < iters;
-            const auto pr = tab.probe(med, cur.h);
-            KeyWords nkw{};
-            u32 e_nn = 0;
-            if (more) {
-                nkw = keyread(e_nxt);
-                e_nn = sst[base + 128 + lane];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            const bool hit = tab.finish(cur.valid, med, k0, k1, cur.h, pr);
-            if (ABL == 3) { sink += hit; cur = decode_tok(e_nxt, base + 64 + lane < total, nkw); e_nxt = e_nn; continue; }
-            my_hits += (u32)hit;
-            store_pending(true);              // the previous iteration's miss units
-            // this token's miss: reserve units in the (workgroup, bucket) region
-            missp = cur.valid && !hit;
-            pp = miss_bucket(cur.h, a.pmask);
-            nup = cur.shrt ? 1u : 2u;
-            posp = atomicAdd(&cursor[pp], missp ? nup : 0u);   // every lane (0 = no miss)
-            k0p = k0; k1p = k1;
-            if (more) {
-                cur = decode_tok(e_nxt, base + 64 + lane < total, nkw);
-                e_nxt = e_nn;
-            }
+        for (u32 it = 0; it < nfs; it++) {
+            const auto pr = tab.probe_short(cs.h);
+            const uint3 nks = keyread_s(e_nxt);
+            const u32 e_nn = ps[64 * (it + 2)];
+            __builtin_amdgcn_sched_barrier(0);  // all three reads issue before the probe's wait
+            const bool hit = tab.finish_short(cs.k, cs.h, pr);
+            hits_w += (u64)__popcll(__ballot(hit));
+            store_pending(false);             // short keys: one unit
+            miss_short(!hit, cs);
+            cs = decode_s(e_nxt, nks);
+            e_nxt = e_nn;
         }
-        if (ABL == 0 || ABL >= 6) store_pending(true);
-        if (ABL) asm volatile("" ::"v"(sink));
+        ncs = ns & 63;
+        for (u32 it = 0; it < nfm; it++) {
+            const auto pr = tab.probe(true, cm.h);
+            const KeyWords nkw = keyread(f_nxt);
+            const u32 f_nn = pm[64 * (it + 2)];
+            __builtin_amdgcn_sched_barrier(0);
+            const bool hit = tab.finish(cm.valid, true, cm.k0, cm.k1, cm.h, pr);
+            hits_w += (u64)__popcll(__ballot(hit));
+            store_pending(true);              // the previous iteration's miss units
+            miss_medium(cm.valid && !hit, cm);
+            cm = decode_m(f_nxt, lm + 64 * (it + 1) < tm, nkw, wbase);
+            f_nxt = f_nn;
+        }
+        ncm = nm & 63;
+        u32 nst = nfs + 2 * nfm;
+        if (nfm) {                            // a medium miss does not stay pending (a short
+            store_pending(true);              // iteration stores one unit)
+            missp = false;
+            nst += 2;
+        }
         wave_lds_sync();
         stamp(5);
         if (WCG_STAMPS) stp[6]++;
-        return (ABL == 0 || ABL >= 6) ? nsh + 2 * (iters + 1) : 0u;
+        return nst;
     };
 
 #else
@@ -1590,6 +1559,21 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
     }
     for (; st < nsteps; st += stride)     // tail steps: byte-exact reloads
         process(st, load_chunk(a.in, a.n, (long)(st * MAP_STEP) - 16 + 16 * lane));
+#if !WCG_DIRECT
+    if (ABL == 0 || ABL >= 6) {           // the carried partial iterations
+        const auto pr = tab.probe_short(cs.h);
+        const auto pm = tab.probe(true, cm.h);
+        const bool vs = (u32)lane < ncs;
+        const bool hs = tab.finish_short_v(vs, cs.k, cs.h, pr);
+        const bool hm = tab.finish(cm.valid, true, cm.k0, cm.k1, cm.h, pm);
+        my_hits += (u32)hs + (u32)hm;
+        store_pending(false);             // pending: a short miss or none
+        miss_short(vs && !hs, cs);
+        store_pending(false);
+        miss_medium(cm.valid && !hm, cm);
+        store_pending(true);
+    }
+#endif
 
     if (WCG_STAMPS && lane == 0)
         for (int i = 0; i < MAP_NSTAMP; i++) atomicAdd((unsigned long long*)&a.stamps[i], (unsigned long long)stp[i]);
@@ -1615,7 +1599,7 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) void k_map(MapArgs 
     // to DevState).  Per-wave atomics on DevState cost ~12 ns each serialised on one line:
     // 16K of them added 0.2 ms to every launch.
     __shared__ u64 wsum[MAP_WAVES][4];
-    u64 v0 = (WCG_DIRECT || lane == 0) ? my_tokens : 0, v1 = my_hits, v2 = my_global, v3 = my_long;
+    u64 v0 = (WCG_DIRECT || lane == 0) ? my_tokens : 0, v1 = my_hits + (lane == 0 ? hits_w : 0), v2 = my_global, v3 = my_long;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         v0 += __shfl_xor(v0, d, 64); v1 += __shfl_xor(v1, d, 64);

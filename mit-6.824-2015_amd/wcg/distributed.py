@@ -6,10 +6,19 @@ Reference semantics being distributed (paths relative to /root/reference):
   * Merge reads every -res-r and sorts all keys (mapreduce.go:284-321).
 Here each rank maps a line-aligned byte range (rank = a group of map jobs), pre-aggregates
 (key, count) on its GPU, exports its records bucketed by owner = (ihash % nReduce) % world
-(partition r is owned by rank r % world), and one all_to_all_single (RCCL grouped
-send/recv over xGMI) delivers every partition to its owner, which reduces it (= DoReduce for
-its partitions: sort + format).  The final Merge sends the owners' sorted runs to rank 0, which
-merges them on its GPU (k-way, by pairwise merge passes).
+(partition r is owned by rank r % world), and the exchange delivers every partition to its
+owner, which reduces it (= DoReduce for its partitions: sort + format).  The final Merge sends
+the owners' sorted runs to rank 0, which merges them on its GPU (k-way, by pairwise merge
+passes).
+
+Two transports carry the exchange and the gather:
+  * the product path (bench.py with backend nccl, after init_comm()): both run inside libwcg -
+    wcg_exchange = ncclAllGather of every rank's status and per-owner record counts, then ONE
+    ncclGroupStart/End of ncclSend/ncclRecv pairs (all-to-all-v over xGMI, each rank's records
+    straight from its export buffer into the owners' import buffers), and wcg_gather_merge =
+    grouped ncclSend/ncclRecv of the sorted runs to rank 0 and its k-way merge;
+  * the portable path (gloo: CPU tests, host-staged rehearsals on one GPU): _exchange() below,
+    torch.distributed all_to_all_single of the counts, then of the records.
 
 The module is device-agnostic: it only needs an engine with export_tensor/import_tensor/reset/
 reduce/result/result_tensor/merge_runs_tensor, so the CPU tests drive it with the `gloo` backend

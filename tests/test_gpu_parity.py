@@ -225,6 +225,33 @@ def test_full_size_c2(built):
     assert st["tokens"] == r.ntokens and nk == r.nkeys
 
 
+@pytest.mark.slow
+def test_full_size_c2_second_job_fused(built):
+    """The headline's reduce path at full size: C2 run as two jobs on one engine,
+    as bench.py's timed steps run it.  The first job takes the multi-launch reduce (no hint yet);
+    the second, with the first job's key count as its hint, takes the one-launch k_fused_reduce
+    (1e5 keys, 1.8e8 tokens) - both merged files byte for byte against the oracle."""
+    import torch
+    import wcg
+    from wcg.corpus import Generator, CONFIGS
+    cfg = CONFIGS["c2_ascii_zipf_1gib"]
+    n = cfg["nbytes"]
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"]).fill_ptr(host.data_ptr(), n)
+    dev = host.to("cuda")
+    data = host.numpy().tobytes()
+    r = ob.Result(data, 16)
+    want = r.merged()
+    with wcg.Engine(0, 0, 1 << 20) as e:
+        for job, path in ((0, 0), (1, 1)):
+            e.reset()
+            e.map_device(dev.data_ptr(), n)
+            nk, nb = e.reduce()
+            assert e.reduce_path() == path, f"job {job}: reduce path {e.reduce_path()}, expected {path}"
+            ob.assert_same(e.result(), want)
+            assert nk == r.nkeys and e.stats()["tokens"] == r.ntokens
+
+
 @pytest.mark.parametrize("shape", ["mixed_16_50", "exactly_16", "runs_100_300"])
 def test_long_token_lengths(built, shape):
     """Inputs made only of long tokens (every step logs dozens): each logged length must be the

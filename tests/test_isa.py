@@ -43,12 +43,14 @@ def test_map_asm_loads_not_copied_before_wait(device_asm):
 
 
 def test_map_unit_stores_unconditional(device_asm):
-    """The prefetch accounting counts 1 miss-log unit store per short-key iteration, 2 per general
-    iteration and 2 after the loops: they must be the inline-asm stores, 5 per inlined copy of the
-    step (four register sets and the tail)."""
+    """The prefetch accounting counts 1 miss-log unit store per short-key iteration, 2 per medium
+    iteration and 2 after a step's last medium iteration (r06: carried tokens): they must be the
+    inline-asm stores issued by the whole wave, 5 per inlined copy of the step (four register
+    sets and the tail), plus the 4 of the drain of the carried tokens after the last step."""
     lines = check_inflight.kernel_lines(device_asm, KMAP0)
     stores = [l for l in lines if "wcg-store" in l]
-    assert stores and all("buffer_store_dwordx2" in l for l in stores) and len(stores) % 5 == 0
+    assert stores and all("buffer_store_dwordx2" in l for l in stores)
+    assert len(stores) == 5 * 5 + 4, len(stores)
 
 
 def test_map_no_scratch(device_asm):
