@@ -45,7 +45,7 @@ constexpr int AGG_PROBES = WCG_AGG_PROBES;
 #endif
 constexpr bool AGG_SPEC_K1 = WCG_AGG_SPEC_K1;
 #ifndef WCG_AGG_ABLATE
-#define WCG_AGG_ABLATE 0       // diagnostics: 1 = loads only, 2 = + decode and hash, 3 = no flush (wrong counts)
+#define WCG_AGG_ABLATE 0       // diagnostics: 1 = loads only, 2 = + decode and hash, 3 = no flush, 4 = short keys only (wrong counts)
 #endif
 
 struct AggArgs {
@@ -58,6 +58,9 @@ struct AggArgs {
     u32 P;                 // pass 1: miss buckets; pass 2: buckets x AGG_Q sub-buckets
     u32 nsrc;              // pass 1: source workgroups of k_map; pass 2: pass-1 slices
     u32 slices;            // workgroups per bucket (pass 2: 1)
+    u32 pm;                // pass 1 (r06): buckets [pm, P) hold medium keys only and take slices_m
+    u32 slices_m;          //   workgroups each (pm = P: no such buckets)
+    u32 nbi;               // (bucket, slice) items: pm * slices + (P - pm) * slices_m
     u32 rstride, rmod;     // region index = w * rstride + b % rmod
     u32 P1;                // pass 2: pass-1 buckets (source w of sub-bucket b: b / AGG_Q + P1 * s)
     int mode;              // AGG_SPILL (pass 1) or AGG_EMIT (pass 2)
@@ -146,10 +149,14 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
     // lanes needs it)
     LdsTable<AGG_NB, u64, AGG_W> tab{tk0, tk1, tcnt};
     constexpr bool emit = MODE == AGG_EMIT;
-    const u32 p = bi % a.P, s = bi / a.P;
+    // item bi -> (bucket p, slice s of sl): the short-key buckets [0, pm) first, slices major,
+    // then the medium-key buckets [pm, P)
+    u32 p, s, sl;
+    if (bi < a.pm * a.slices) { p = bi % a.pm; s = bi / a.pm; sl = a.slices; }
+    else { const u32 b2 = bi - a.pm * a.slices, nm = a.P - a.pm; p = a.pm + b2 % nm; s = b2 / nm; sl = a.slices_m; }
     u32 k0_, k1_, wbase, wstep;
     if (!emit) {
-        k0_ = (u32)(((u64)a.nsrc * s) / a.slices); k1_ = (u32)(((u64)a.nsrc * (s + 1)) / a.slices);
+        k0_ = (u32)(((u64)a.nsrc * s) / sl); k1_ = (u32)(((u64)a.nsrc * (s + 1)) / sl);
         wbase = 0; wstep = 1;
     } else {
         k0_ = 0; k1_ = a.nsrc;
@@ -251,6 +258,10 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
         bool v[4];
         u32 nu[4];
         agg_decode(u, k0, k1, c, v, nu);
+        if (WCG_AGG_ABLATE == 4) {            // diagnostics: short keys only (medium entries dropped)
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = v[j] && key_short(k0[j]);
+        }
         if (WCG_AGG_ABLATE == 2) {
             u32 x = 0;
 #pragma unroll
@@ -438,7 +449,7 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
     __shared__ u32 spos;                       // pass 1: spill cursor
     __shared__ u64 wsum[AGG_NT / 64][4];       // per-wave sums (the record log's counts, stats)
     const int tid = threadIdx.x;
-    const u32 nb = a.P * a.slices;
+    const u32 nb = a.nbi;
     const u64 t0 = a.clk ? wall_clock64() : 0;
     // one-pass map calls: compaction's counters start at zero (its memset dispatch cost ~4 us)
     if (MODE == AGG_SPILL && blockIdx.x == 0 && tid == 0) { a.st->nrec = 0; a.st->nlong = 0; }

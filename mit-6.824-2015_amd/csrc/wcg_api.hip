@@ -131,7 +131,6 @@ struct wcg_ctx {
     // long-token log (k_map -> k_long): one region of {offset | len << 40} records per workgroup
     u64* llog = nullptr; u64 llog_cap = 0;
     u32* llog_len = nullptr; u64 llog_len_cap = 0;
-    u32 nbuckets = 64;                                // miss buckets P (<= MAX_MISS_BUCKETS)
     // ingest (wcg_ingest.h): two pinned staging buffers, two device buffers, a reader pool
     u64 chunk = 64ull << 20;
     uint8_t* hb[INGEST_SLOTS] = {};
@@ -1265,8 +1264,10 @@ int agg_clock_report(wcg_ctx* c, const AggArgs& g, u32 nb1, u64 grid) {
     u32 bmax = 0;
     std::vector<u64> units(nb1, 0);
     for (u32 bi = 0; bi < nb1; bi++) {
-        const u32 p = bi % g.P, s = bi / g.P;
-        const u32 k0 = (u32)((grid * s) / g.slices), k1 = (u32)((grid * (s + 1)) / g.slices);
+        u32 p, s, sl;                     // as agg_one
+        if (bi < g.pm * g.slices) { p = bi % g.pm; s = bi / g.pm; sl = g.slices; }
+        else { const u32 b2 = bi - g.pm * g.slices, nm = g.P - g.pm; p = g.pm + b2 % nm; s = b2 / nm; sl = g.slices_m; }
+        const u32 k0 = (u32)((grid * s) / sl), k1 = (u32)((grid * (s + 1)) / sl);
         for (u32 k = k0; k < k1; k++) units[bi] += rl[(u64)k * g.P + p];
         const double d = (double)(clk[2 * bi + 1] - clk[2 * bi]);
         sd += d; su += (double)units[bi];
@@ -1330,12 +1331,21 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // bytes: a unit for every 4 input bytes covers every token missing the LDS table even on
     // high-cardinality UTF-8 text (C4: 0.1 tokens per byte, 79% misses, 2-unit keys), where a
     // 1-per-8 pool overflowed into per-token global-table inserts; only written units cost time
-    const u32 P = c->nbuckets;
-    static_assert(MAX_MISS_BUCKETS >= 64, "k_map's LDS cursors cover the 64 miss buckets");
+    // miss buckets: one-pass jobs (r06) log short keys (<= 7 bytes) and medium keys to disjoint
+    // halves, so that every k_agg workgroup aggregates one kind only (a wave that mixed them paid the
+    // medium keys' dependent k1 reads on nearly every probe: C2 k_agg with medium entries dropped ran
+    // 0.197 ms against 0.270, profiles/r06_experiments); two-pass jobs keep one set of buckets
+    static const char* tp_env0 = getenv("WCG_AGG_TWO_PASS");
+    const bool two_pass0 = tp_env0 ? atoi(tp_env0) != 0 : c->max_keys > (4ull << 20);
+    static const char* sp_env = getenv("WCG_AGG_SPLIT");       // measurement: 0 = one set of buckets
+    const bool split = !two_pass0 && !(sp_env && atoi(sp_env) == 0);
+    const u32 P = split ? MISS_SHORT_BUCKETS + MISS_SHORT_BUCKETS / 2 : MISS_SHORT_BUCKETS;   // short, then medium
+    static_assert(MISS_SHORT_BUCKETS + MISS_SHORT_BUCKETS / 2 <= MAX_MISS_BUCKETS, "k_map's LDS cursors cover P");
     u64 per_wg_bytes = (u64)a.tiles_per_wg * MAP_STEP;
     // even (16-byte aligned regions); a workgroup's regions stay under 2 GiB so k_map's unit
     // offsets fit 32 bits and its 24-bit multiplies (P * region_cap * 8 <= 2^31)
-    a.region_cap = std::min<u64>(std::max<u64>(2048, per_wg_bytes / (4ull * P)), (1ull << 31) / (8ull * P)) & ~1ull;
+    // (split buckets: every region sized like an unsplit bucket's)
+    a.region_cap = std::min<u64>(std::max<u64>(2048, per_wg_bytes / (4ull * MISS_SHORT_BUCKETS)), (1ull << 31) / (8ull * P)) & ~1ull;
     a.pmask = P - 1;
     u64 need = (grid * P * a.region_cap + AGG_SLACK_UNITS) * sizeof(u64);
     if (need > c->pool_bytes) {
@@ -1385,8 +1395,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // record-log merge would only cost time.  One pass sends an entry its LDS table cannot take
     // to the global table.  Two-pass jobs keep the global table empty: pass 2's records, its
     // overflow and k_long_hash's inline runs all go to the record log.
-    static const char* tp_env = getenv("WCG_AGG_TWO_PASS");
-    const bool two_pass = tp_env ? atoi(tp_env) != 0 : c->max_keys > (4ull << 20);
+    const bool two_pass = two_pass0;
     const u64 rec_cap_emit = c->max_keys + 65536;
     RC(ensure(c, &c->remit, &c->remit_cap, rec_cap_emit));
     a.emit = two_pass ? c->remit : nullptr;
@@ -1411,14 +1420,14 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         else kern<<<(unsigned)grid, MAP_NT, 0, c->stream>>>(a);
     };
     switch (ablate) {
-        case 1: launch(k_map<1>); break;
-        case 2: launch(k_map<2>); break;
-        case 3: launch(k_map<3>); break;
-        case 4: launch(k_map<4>); break;
-        case 5: launch(k_map<5>); break;
-        case 6: launch(k_map<6>); break;
-        case 7: launch(k_map<7>); break;
-        default: launch(k_map<0>); break;
+        case 1: split ? launch(k_map<1, true>) : launch(k_map<1, false>); break;
+        case 2: split ? launch(k_map<2, true>) : launch(k_map<2, false>); break;
+        case 3: split ? launch(k_map<3, true>) : launch(k_map<3, false>); break;
+        case 4: split ? launch(k_map<4, true>) : launch(k_map<4, false>); break;
+        case 5: split ? launch(k_map<5, true>) : launch(k_map<5, false>); break;
+        case 6: split ? launch(k_map<6, true>) : launch(k_map<6, false>); break;
+        case 7: split ? launch(k_map<7, true>) : launch(k_map<7, false>); break;
+        default: split ? launch(k_map<0, true>) : launch(k_map<0, false>); break;
     }
     HIPCHK(c, hipGetLastError());
 #if WCG_STAMPS
@@ -1482,12 +1491,26 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     AggArgs g;
     g.pool = c->pool; g.region_len = c->region_len; g.region_cap = a.region_cap;
     g.P = P; g.nsrc = (u32)grid;
-    g.slices = std::max<u32>(1, std::min<u32>((u32)grid, (u32)(c->ncu + P - 1) / P));
-    g.slices = std::max<u32>(g.slices, (u32)((grid + AGG_MAX_SRC - 1) / AGG_MAX_SRC));
+    const u32 min_sl = (u32)((grid + AGG_MAX_SRC - 1) / AGG_MAX_SRC);   // <= AGG_MAX_SRC regions per item
+    if (split) {
+        // the medium buckets (~11% of C2's tokens, ~1/4 of the units) a quarter of the CUs, the
+        // short buckets the rest: ~one workgroup per CU of ~equal time
+        g.pm = MISS_SHORT_BUCKETS;
+        const u32 nm = P - g.pm;
+        g.slices_m = std::max<u32>(min_sl, std::max<u32>(1, std::min<u32>((u32)grid, (u32)c->ncu / 4 / nm)));
+        g.slices = std::max<u32>(min_sl, std::max<u32>(1, std::min<u32>((u32)grid,
+                                 (u32)(c->ncu > g.slices_m * nm ? (c->ncu - g.slices_m * nm) / g.pm : 1))));
+    } else {
+        g.pm = P;
+        g.slices_m = 1;
+        g.slices = std::max<u32>(1, std::min<u32>((u32)grid, (u32)(c->ncu + P - 1) / P));
+        g.slices = std::max<u32>(g.slices, min_sl);
+    }
+    g.nbi = g.pm * g.slices + (P - g.pm) * g.slices_m;
     g.rstride = P; g.rmod = P; g.P1 = P; g.mode = AGG_SPILL;
     g.gtab = c->gtab; g.gmask = c->gslots - 1; g.st = c->st;
     g.map_stats = c->wg_stats;
-    const u32 nb1 = P * g.slices;
+    const u32 nb1 = g.nbi;
     g.spill_cap = 0;                      // one pass: a full LDS table inserts into the global table
     g.spill = nullptr; g.spill_len = nullptr;
     g.emit = c->remit; g.emit_cap = rec_cap_emit;
@@ -1535,6 +1558,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     AggArgs g2 = g;
     g2.pool = c->pool2; g2.region_len = c->rlen2; g2.region_cap = cap2;
     g2.P = P * AGG_Q; g2.nsrc = sl; g2.slices = 1;
+    g2.pm = g2.P; g2.slices_m = 1; g2.nbi = g2.P;
     g2.rstride = AGG_Q; g2.rmod = AGG_Q; g2.P1 = P; g2.mode = AGG_EMIT;
     const u32 grid2 = std::min<u32>(P * AGG_Q, (u32)c->ncu * 2);
     g2.ovf_cap = AGG_OVF_CAP;

@@ -18,6 +18,9 @@
 #ifndef WCG_DIAG_SLOTS
 #define WCG_DIAG_SLOTS 0
 #endif
+#ifndef WCG_MAP_ROW2
+#define WCG_MAP_ROW2 0                       // k_map short keys: one 2-slot row instead of two choices
+#endif
 #ifndef WCG_DIAG_NOCOUNT
 #define WCG_DIAG_NOCOUNT 0                   // diagnostics: 1 = k_map's short-key hits not counted
 #endif
@@ -238,8 +241,17 @@ struct MapTable {
     struct ProbeS { u32 s1, s2; u64 x1, x2; };
     __device__ __forceinline__ ProbeS probe_short(u32 h) const {
         ProbeS p;
+#if WCG_MAP_ROW2
+        // one choice of a 16-byte row of two slots: one ds_read_b128, one slot multiply
+        static_assert(NS % 2 == 0, "rows of two short slots");
+        p.s1 = 2 * (u32)(((u64)(h >> 8) * (u64)((NS / 2) << 8)) >> 32);
+        p.s2 = p.s1 + 1;
+        const uint4 r = *reinterpret_cast<const uint4*>(sk0 + p.s1);
+        p.x1 = (u64)r.y << 32 | r.x; p.x2 = (u64)r.w << 32 | r.z;
+#else
         slots(h, (u32)NS, p.s1, p.s2);
         p.x1 = sk0[p.s1]; p.x2 = sk0[p.s2];
+#endif
         return p;
     }
     __device__ __forceinline__ bool finish_short(u64 a0, u32 h, const ProbeS& p) {

@@ -12,14 +12,15 @@
 //      F2), Go UTF-8 decode + Unicode-13 letter bitmap otherwise (fact F1));
 //   3. token starts = letter & ~prev_letter (fact F3) with the neighbour chunks' masks taken by
 //      DPP lane shifts; each start's run length is read off the 32-bit mask window (own | next);
-//      the wave compacts {offset, length} entries (prefix sum from 4 ballots + mbcnt) into its
-//      LDS list;
-//   4. tokens, 64 per uniform iteration: key identity (<= 15 bytes, fact F4) from three aligned
-//      8-byte LDS reads -> the workgroup's LDS tables (exact keys, short and medium keys in
-//      2-choice x 1-slot tables, u32 counts: MapTable); a miss is appended to this workgroup's
-//      region of the miss log for k_agg; tokens > 15 bytes go to the long-key table with an
-//      arena copy of their bytes (global memory path);
-//   5. at the end the workgroup flushes its LDS table into the miss log too.
+//      the wave compacts {offset, length} entries into two LDS lists, short keys (<= 7 bytes)
+//      and the others (one DPP prefix sum gives every lane both list offsets);
+//   4. tokens, 64 per uniform iteration, the short list then the other: key identity (<= 15
+//      bytes, fact F4) from aligned dword LDS reads -> the workgroup's LDS tables (exact keys,
+//      u32 counts: MapTable); a miss is appended to this workgroup's region of the miss log for
+//      k_agg; a token > 15 bytes is logged for k_long_hash / k_long_small.  A list's partial last
+//      iteration is carried in registers into the next step's first iteration (r06);
+//   5. after its last step the wave runs its carried tokens, and the workgroup flushes its LDS
+//      table into the miss log too.
 // Token ownership: a token belongs to the 16-byte chunk holding its first byte (exactly once);
 // only lanes 1-62 own chunks.
 //
@@ -64,7 +65,7 @@ constexpr int MAP_SST = 512;                 // max token starts per step (992 /
 // table 4.3 KiB); without the start list the window staging (16 x 1032 B) and the lists
 // (16 x 1 KiB) are free for 2736 more
 #ifndef WCG_MAP_NS
-#define WCG_MAP_NS ((WCG_ADMIT2 ? 8432 : 8624) + (WCG_DIRECT ? 2736 : 0))
+#define WCG_MAP_NS ((WCG_ADMIT2 ? 8410 : 8602) + (WCG_DIRECT ? 2736 : 0))   // (r06: 22 fewer for 64 more cursors)
 #endif
 #ifndef WCG_MAP_NM
 #define WCG_MAP_NM 1024
@@ -86,7 +87,18 @@ constexpr int MAP_SETS = WCG_MAP_SETS;       // steps in flight per wave (2 or 4
 #endif
 constexpr int MAP_NSTAMP = 7;                // {loop, window wait, staging+mask, start list, short loop,
                                              //  general loop, steps}
-constexpr int MAX_MISS_BUCKETS = 64;         // miss buckets P (the host uses 64)
+constexpr int MAX_MISS_BUCKETS = 128;        // miss buckets P (the host uses 64 + 32, or 64)
+// A key's miss bucket (k_map<ABL, SPLIT>, r06): one-pass jobs (SPLIT) log short keys (<= 7 bytes)
+// to buckets 0-63 and medium keys to 64-95, so that every k_agg workgroup aggregates one kind (a
+// wave that mixed them paid the medium keys' dependent k1 reads on nearly every probe); 32 medium
+// buckets, not 64: a medium region then fills at half a short one's rate (64 left partial lines
+// for the L2 to write back, +9% WRITE_SIZE).  Two-pass jobs keep 64 buckets of both kinds.  The
+// bucket maps are compile-time constants: as kernel arguments they cost k_map SGPR spills (+2.5%).
+constexpr u32 MISS_SHORT_BUCKETS = 64;
+template <bool SPLIT> __device__ __forceinline__ u32 short_bucket(u32 h) { return h & (MISS_SHORT_BUCKETS - 1); }
+template <bool SPLIT> __device__ __forceinline__ u32 medium_bucket(u32 h) {
+    return SPLIT ? (h & (MISS_SHORT_BUCKETS / 2 - 1)) + MISS_SHORT_BUCKETS : (h & (MISS_SHORT_BUCKETS - 1));
+}
 constexpr u32 SST_LEN_SHIFT = 10;            // start entry = window offset | min(run, 16) << 10
 
 struct MapArgs {
@@ -908,7 +920,8 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 x) {
 
 // ABL (measurement builds only, selected by WCG_MAP_ABLATE; results are wrong when ABL != 0):
 //   5 = input loads only, 4 = + LDS staging and letter masks, 1 = + token starts and compaction,
-//   2 = + key extraction and hash, 3 = + LDS lookup with misses dropped; 6 = full but long
+//   2 = + the per-step decode of both lists' first tokens, 3 = + the short-key iterations' probes
+//   and decodes (no table update, no miss; medium iterations in full); 6 = full but long
 //   tokens only counted, 7 = full but long tokens only measured and hashed
 // ---- r04: the letter mask of a wave's window with non-ASCII bytes, by a wave-wide list of the
 //      UTF-8 leads.  The lead-compacted form (utf8_mask_lds) decodes eight lead slots per lane,
@@ -1006,7 +1019,7 @@ __device__ __forceinline__ u32 utf8_mask_list(uint4 c, u32 nx, LdsLetters lt, co
     return wm[lane];
 }
 
-template <int ABL>
+template <int ABL, bool SPLIT>
 #if WCG_MAP_WGS > 1
 // occupancy experiments (r06): 8 waves per SIMD also needs <= 80 SGPRs
 #define WCG_MAP_ATTR __attribute__((amdgpu_waves_per_eu(4 * WCG_MAP_WGS * WCG_MAP_NT / 1024, 4 * WCG_MAP_WGS * WCG_MAP_NT / 1024)))
@@ -1164,14 +1177,14 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) WCG_MAP_ATTR void k
     };
     auto miss_short = [&](bool miss, const TokS& t) {
         missp = miss;
-        pp = miss_bucket(t.h, a.pmask);
+        pp = short_bucket<SPLIT>(t.h);
         nup = 1u;
         posp = atomicAdd(&cursor[pp], miss ? 1u : 0u);   // every lane (0 = no miss)
         k0p = t.k; k1p = 0;
     };
     auto miss_medium = [&](bool miss, const TokM& t) {
         missp = miss;
-        pp = miss_bucket(t.h, a.pmask);
+        pp = medium_bucket<SPLIT>(t.h);
         nup = 2u;
         posp = atomicAdd(&cursor[pp], miss ? 2u : 0u);
         k0p = t.k0; k1p = t.k1;
@@ -1254,7 +1267,7 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) WCG_MAP_ATTR void k
         wave_lds_sync();
         stamp(3);
         my_tokens += total;
-        if (ABL >= 1 && ABL <= 3) return 0;   // (r06: levels 2 and 3 are level 1)
+        if (ABL == 1) return 0;
 
         // ---- tokens: uniform iterations of 64 tokens, the short list first, then the medium/long
         //      one, each software-pipelined so that one LDS round trip per iteration carries this
@@ -1282,11 +1295,18 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) WCG_MAP_ATTR void k
             if ((u32)lane >= ncm) cm = u;
         }
         stamp(4);
+        if (ABL == 2) { asm volatile("" ::"v"(cs.h), "v"(cm.h), "v"(e_nxt), "v"(f_nxt)); ncs = ns & 63; ncm = nm & 63; return 0; }
         for (u32 it = 0; it < nfs; it++) {
             const auto pr = tab.probe_short(cs.h);
             const uint3 nks = keyread_s(e_nxt);
             const u32 e_nn = ps[64 * (it + 2)];
             __builtin_amdgcn_sched_barrier(0);  // all three reads issue before the probe's wait
+            if (ABL == 3) {                   // probe reads and decodes, no table update or miss
+                asm volatile("" ::"v"(pr.x1), "v"(pr.x2));
+                cs = decode_s(e_nxt, nks);
+                e_nxt = e_nn;
+                continue;
+            }
             const bool hit = tab.finish_short(cs.k, cs.h, pr);
             hits_w += (u64)__popcll(__ballot(hit));
             store_pending(false);             // short keys: one unit
@@ -1440,7 +1460,7 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) WCG_MAP_ATTR void k
                 my_hits += (u32)hit;
                 store_pending(false);
                 missp = v && !hit;
-                pp = miss_bucket(t.h, a.pmask);
+                pp = short_bucket<SPLIT>(t.h);
                 nup = 1u;
                 posp = atomicAdd(&cursor[pp], missp ? 1u : 0u);
                 k0p = t.k; k1p = 0;
@@ -1478,7 +1498,7 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) WCG_MAP_ATTR void k
                 my_hits += (u32)hit;
                 store_pending(true);
                 missp = val && !hit;
-                pp = miss_bucket(t.h, a.pmask);
+                pp = medium_bucket<SPLIT>(t.h);
                 nup = 2u;
                 posp = atomicAdd(&cursor[pp], missp ? 2u : 0u);
                 k0p = t.k0; k1p = t.k1;
@@ -1582,7 +1602,8 @@ __global__ __launch_bounds__(MAP_NT, MAP_WGS * MAP_NT / 256) WCG_MAP_ATTR void k
     __syncthreads();
     auto flush = [&](u64 k0, u64 k1, u32 c) {
         if (!c) return;
-        if (!log_push(a, cursor, miss_bucket(lds_hash(k0, k1), a.pmask), k0, k1, c)) {
+        const u32 h = lds_hash(k0, k1);
+        if (!log_push(a, cursor, key_short(k0) ? short_bucket<SPLIT>(h) : medium_bucket<SPLIT>(h), k0, k1, c)) {
             my_global++;
             ginsert(a.gtab, a.gmask, k0, k1, gslot(key_hash(k0, k1)), c, a.st);
         }

@@ -19,7 +19,9 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import check_inflight  # noqa: E402
 
-KMAP0 = "_ZN3wcg5k_mapILi0EEEvNS_7MapArgsE"
+# k_map<0, SPLIT>: one-pass jobs log short and medium keys to separate miss buckets (SPLIT), two-pass
+# jobs to one set; both instances carry the same discipline
+KMAPS = ["_ZN3wcg5k_mapILi0ELb1EEEvNS_7MapArgsE", "_ZN3wcg5k_mapILi0ELb0EEEvNS_7MapArgsE"]
 
 
 @pytest.fixture(scope="module")
@@ -33,8 +35,9 @@ def device_asm(tmp_path_factory):
     return out.read_text()
 
 
-def test_map_asm_loads_not_copied_before_wait(device_asm):
-    errors, loads, waits = check_inflight.check(device_asm, KMAP0)
+@pytest.mark.parametrize("kmap", KMAPS)
+def test_map_asm_loads_not_copied_before_wait(device_asm, kmap):
+    errors, loads, waits = check_inflight.check(device_asm, kmap)
     assert not errors, errors
     sets = "ABCD"
     assert set(loads) == {s + "0" for s in sets}
@@ -42,17 +45,19 @@ def test_map_asm_loads_not_copied_before_wait(device_asm):
     assert sorted({w[0] for w in waits}) == list(sets) and len(waits) >= 2 * len(sets)
 
 
-def test_map_unit_stores_unconditional(device_asm):
+@pytest.mark.parametrize("kmap", KMAPS)
+def test_map_unit_stores_unconditional(device_asm, kmap):
     """The prefetch accounting counts 1 miss-log unit store per short-key iteration, 2 per medium
     iteration and 2 after a step's last medium iteration (r06: carried tokens): they must be the
     inline-asm stores issued by the whole wave, 5 per inlined copy of the step (four register
     sets and the tail), plus the 4 of the drain of the carried tokens after the last step."""
-    lines = check_inflight.kernel_lines(device_asm, KMAP0)
+    lines = check_inflight.kernel_lines(device_asm, kmap)
     stores = [l for l in lines if "wcg-store" in l]
     assert stores and all("buffer_store_dwordx2" in l for l in stores)
     assert len(stores) == 5 * 5 + 4, len(stores)
 
 
-def test_map_no_scratch(device_asm):
-    lines = check_inflight.kernel_lines(device_asm, KMAP0)
+@pytest.mark.parametrize("kmap", KMAPS)
+def test_map_no_scratch(device_asm, kmap):
+    lines = check_inflight.kernel_lines(device_asm, kmap)
     assert not any(re.search(r"\bscratch_(load|store)", l) for l in lines)
