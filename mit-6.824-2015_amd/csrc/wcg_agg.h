@@ -24,6 +24,7 @@
 #pragma once
 #include "wcg_common.h"
 #include "wcg_lds_table.h"
+#include "wcg_map.h"
 
 namespace wcg {
 
@@ -61,6 +62,8 @@ struct AggArgs {
     u32 pm;                // pass 1 (r06): buckets [pm, P) hold medium keys only and take slices_m
     u32 slices_m;          //   workgroups each (pm = P: no such buckets)
     u32 nbi;               // (bucket, slice) items: pm * slices + (P - pm) * slices_m
+    u32 ls_nreg;           // pass 1 (r06): workgroup nbi (the grid's last) runs long_small over
+                           //   ls_nreg map regions (wcg_map.h; 0: no such workgroup)
     u32 rstride, rmod;     // region index = w * rstride + b % rmod
     u32 P1;                // pass 2: pass-1 buckets (source w of sub-bucket b: b / AGG_Q + P1 * s)
     int mode;              // AGG_SPILL (pass 1) or AGG_EMIT (pass 2)
@@ -141,7 +144,7 @@ WCG_AGG_SET_OPS(C)
 // MODE is a template parameter: one kernel for both passes held the union of their registers
 // (128 VGPRs with a spill)
 template <int MODE>
-__device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[AGG_W], u64 (*tcnt)[AGG_W], u32* rlen_s,
+__device__ __forceinline__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[AGG_W], u64 (*tcnt)[AGG_W], u32* rlen_s,
                        u32* bstart, u32& spos, u64 (*wsum)[4]) {
     const int tid = threadIdx.x;
     // (a first-fit variant that reads b2's row only when b1 is full - half the LDS bytes - measured
@@ -439,17 +442,32 @@ __device__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[A
 // pass 1: one workgroup per (bucket, slice); pass 2: a persistent grid over the sub-buckets (most
 // are empty on low-cardinality text, and an empty one costs a few LDS reads instead of a launch
 // of a 160 KiB workgroup)
+struct AggTabs {
+    u64 tk0[AGG_NB][AGG_W];
+    u64 tk1[AGG_NB][AGG_W];
+    u64 tcnt[AGG_NB][AGG_W];
+};
+union AggLds {
+    AggTabs t;
+    LsLds ls;
+};
+static_assert(LS_NT == AGG_NT, "long_small runs as a k_agg workgroup");
 template <int MODE>
-__global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a) {
-    __shared__ __align__(16) u64 tk0[AGG_NB][AGG_W];
-    __shared__ __align__(16) u64 tk1[AGG_NB][AGG_W];
-    __shared__ u64 tcnt[AGG_NB][AGG_W];
+__global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a, MapArgs ma) {
+    __shared__ __align__(16) AggLds lds;
+    u64 (*const tk0)[AGG_W] = lds.t.tk0;
+    u64 (*const tk1)[AGG_W] = lds.t.tk1;
+    u64 (*const tcnt)[AGG_W] = lds.t.tcnt;
     __shared__ u32 rlen_s[AGG_MAX_SRC];
     __shared__ u32 bstart[AGG_MAX_SRC + 1];
     __shared__ u32 spos;                       // pass 1: spill cursor
     __shared__ u64 wsum[AGG_NT / 64][4];       // per-wave sums (the record log's counts, stats)
     const int tid = threadIdx.x;
     const u32 nb = a.nbi;
+    if (MODE == AGG_SPILL && a.ls_nreg && blockIdx.x == nb) {
+        long_small(ma, a.ls_nreg, lds.ls);
+        return;
+    }
     const u64 t0 = a.clk ? wall_clock64() : 0;
     // one-pass map calls: compaction's counters start at zero (its memset dispatch cost ~4 us)
     if (MODE == AGG_SPILL && blockIdx.x == 0 && tid == 0) { a.st->nrec = 0; a.st->nlong = 0; }

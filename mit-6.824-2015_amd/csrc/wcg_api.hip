@@ -872,7 +872,7 @@ int ingest_init(wcg_ctx* c) {
     return WCG_OK;
 }
 
-// long tokens of the previous job up to which a one-pass map call runs k_long_small
+// long tokens of the previous job up to which a one-pass map call runs long_small (k_agg)
 constexpr u64 LONG_SMALL_MAX = 4096;
 
 // a byte after which no rune and no token continues: an ASCII byte that is not a letter
@@ -1261,6 +1261,8 @@ int agg_clock_report(wcg_ctx* c, const AggArgs& g, u32 nb1, u64 grid) {
     u64 t0 = ~0ull, t1 = 0;
     for (u32 b = 0; b < nb1; b++) { t0 = std::min(t0, clk[2 * b]); t1 = std::max(t1, clk[2 * b + 1]); }
     double sd = 0, su = 0, md = 0, mu = 0;
+    double kd[2] = {0, 0}, km[2] = {0, 0}, ku[2] = {0, 0};   // short / medium buckets (split jobs)
+    u32 kn[2] = {0, 0};
     u32 bmax = 0;
     std::vector<u64> units(nb1, 0);
     for (u32 bi = 0; bi < nb1; bi++) {
@@ -1273,7 +1275,13 @@ int agg_clock_report(wcg_ctx* c, const AggArgs& g, u32 nb1, u64 grid) {
         sd += d; su += (double)units[bi];
         if (d > md) { md = d; bmax = bi; }
         mu = std::max(mu, (double)units[bi]);
+        const int kind = bi >= g.pm * g.slices;
+        kd[kind] += d; km[kind] = std::max(km[kind], d); ku[kind] += (double)units[bi]; kn[kind]++;
     }
+    for (int kind = 0; kind < 2; kind++)
+        if (kn[kind])
+            fprintf(stderr, "wcg k_agg clock: %s workgroups %u, dur mean %.1f max %.1f us, units mean %.0f\n",
+                    kind ? "medium" : "short", kn[kind], kd[kind] / kn[kind] / 100.0, km[kind] / 100.0, ku[kind] / kn[kind]);
     fprintf(stderr, "wcg k_agg clock: span %.1f us, wg dur mean %.1f max %.1f us (bi %u: %llu units, start +%.1f us), "
             "units mean %.0f max %.0f\n", (t1 - t0) / 100.0, sd / nb1 / 100.0, md / 100.0, bmax,
             (unsigned long long)units[bmax], (clk[2 * bmax] - t0) / 100.0, su / nb1, mu);
@@ -1460,13 +1468,12 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
         HIPCHK(c, hipStreamWaitEvent(c->long_stream, c->ev_fork, 0));
     }
-    // one-pass calls after a job with few long tokens: one small workgroup does it all
+    // one-pass calls after a job with few long tokens: one workgroup (k_agg's last) does it all
     static const char* ls_env = getenv("WCG_LONG_SMALL");        // measurement: 0 = never, 1 = always
     const bool small = long_path && !two_pass && grid <= LS_MAXREG &&
                        (ls_env ? atoi(ls_env) != 0 : c->long_hint <= LONG_SMALL_MAX);
     if (small) {
-        k_long_small<<<1, LS_NT, 0, ls>>>(a, (u32)grid);
-        HIPCHK(c, hipGetLastError());
+        // (run by k_agg's last workgroup, below)
     } else if (long_path) {
         LongPart lp;
         const u64 expect = grid * (u64)a.tiles_per_wg * 16;     // 16 per step: 3x C4's rate
@@ -1497,7 +1504,9 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         // short buckets the rest: ~one workgroup per CU of ~equal time
         g.pm = MISS_SHORT_BUCKETS;
         const u32 nm = P - g.pm;
-        g.slices_m = std::max<u32>(min_sl, std::max<u32>(1, std::min<u32>((u32)grid, (u32)c->ncu / 4 / nm)));
+        static const char* ms_env = getenv("WCG_AGG_MSLICES");   // measurement: medium slices
+        g.slices_m = std::max<u32>(min_sl, std::max<u32>(1, std::min<u32>((u32)grid,
+                                   ms_env ? (u32)atoi(ms_env) : (u32)c->ncu / 4 / nm)));
         g.slices = std::max<u32>(min_sl, std::max<u32>(1, std::min<u32>((u32)grid,
                                  (u32)(c->ncu > g.slices_m * nm ? (c->ncu - g.slices_m * nm) / g.pm : 1))));
     } else {
@@ -1507,6 +1516,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         g.slices = std::max<u32>(g.slices, min_sl);
     }
     g.nbi = g.pm * g.slices + (P - g.pm) * g.slices_m;
+    g.ls_nreg = small ? (u32)grid : 0u;
     g.rstride = P; g.rmod = P; g.P1 = P; g.mode = AGG_SPILL;
     g.gtab = c->gtab; g.gmask = c->gslots - 1; g.st = c->st;
     g.map_stats = c->wg_stats;
@@ -1530,7 +1540,7 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
         g.clk = nb1 <= 65536 ? d_clk : nullptr;
     }
     if (!two_pass) {
-        k_agg<AGG_SPILL><<<nb1, AGG_NT, 0, c->stream>>>(g);
+        k_agg<AGG_SPILL><<<nb1 + (small ? 1 : 0), AGG_NT, 0, c->stream>>>(g, a);
         HIPCHK(c, hipGetLastError());
         c->counts_clean = true;                // its block 0 zeroed nrec / nlong
         if (g.clk) RC(agg_clock_report(c, g, nb1, grid));
@@ -1564,7 +1574,8 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     g2.ovf_cap = AGG_OVF_CAP;
     RC(ensure(c, &c->ovf, &c->ovf_cap, (u64)grid2 * AGG_OVF_CAP));
     g2.ovf = c->ovf;
-    k_agg<AGG_EMIT><<<grid2, AGG_NT, 0, c->stream>>>(g2);
+    g2.ls_nreg = 0;
+    k_agg<AGG_EMIT><<<grid2, AGG_NT, 0, c->stream>>>(g2, a);
     HIPCHK(c, hipGetLastError());
     }
     if (fork) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));

@@ -17,7 +17,7 @@
 //   4. tokens, 64 per uniform iteration, the short list then the other: key identity (<= 15
 //      bytes, fact F4) from aligned dword LDS reads -> the workgroup's LDS tables (exact keys,
 //      u32 counts: MapTable); a miss is appended to this workgroup's region of the miss log for
-//      k_agg; a token > 15 bytes is logged for k_long_hash / k_long_small.  A list's partial last
+//      k_agg; a token > 15 bytes is logged for k_long_hash / long_small.  A list's partial last
 //      iteration is carried in registers into the next step's first iteration (r06);
 //   5. after its last step the wave runs its carried tokens, and the workgroup flushes its LDS
 //      table into the miss log too.
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(LA_NT) void k_long_agg(MapArgs a, LongPart lp) {
     }
 }
 
-// k_long_small: the long-key work of a one-pass map call with few long tokens, in ONE workgroup
+// long_small: the long-key work of a one-pass map call with few long tokens, in ONE workgroup
 // (C2 logs ~200 long tokens per GiB; k_long_hash + k_long_agg, a 1024-workgroup and a
 // 256-workgroup launch that nearly all find nothing to do, took 17.5 us per step: r05 trace).
 // Rounds of LS_NT logged tokens over every region (a region found by binary search over the
@@ -758,11 +758,21 @@ __global__ __launch_bounds__(LA_NT) void k_long_agg(MapArgs a, LongPart lp) {
 constexpr int LS_NT = 1024;
 constexpr u32 LS_SLOTS = 2048;
 constexpr u32 LS_MAXREG = LS_NT;              // map regions (one length per thread)
-__global__ __launch_bounds__(LS_NT) void k_long_small(MapArgs a, u32 nreg) {
-    __shared__ u64 stag[LS_SLOTS], srec[LS_SLOTS], scnt[LS_SLOTS];
-    __shared__ uint4 sw[LS_SLOTS][2];
-    __shared__ u32 rpre[LS_MAXREG + 1];
-    __shared__ u32 ls_ws[LS_NT / 64];
+struct LsLds {
+    u64 stag[LS_SLOTS], srec[LS_SLOTS], scnt[LS_SLOTS];
+    u32 sw[LS_SLOTS][8];
+    u32 rpre[LS_MAXREG + 1];
+    u32 ws[LS_NT / 64];
+};
+// r06: run by the last workgroup of k_agg's one-pass launch (lds: k_agg's table memory), which
+// starts on the first CU a k_agg workgroup leaves: the separate one-workgroup launch and its
+// dependency cost ~15 us of every C2 step
+__device__ __forceinline__ void long_small(const MapArgs& a, u32 nreg, LsLds& L) {
+    u64* const stag = L.stag;
+    u64* const srec = L.srec;
+    u64* const scnt = L.scnt;
+    u32* const rpre = L.rpre;
+    u32* const ls_ws = L.ws;
     const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (u32 s = tid; s < LS_SLOTS; s += LS_NT) { stag[s] = 0; srec[s] = 0; scnt[s] = 0; }
     // the regions' record counts (clamped to the log: a fuller region was flagged by k_map) and
@@ -810,8 +820,8 @@ __global__ __launch_bounds__(LS_NT) void k_long_small(MapArgs a, u32 nreg) {
                     t = atomicCAS((unsigned long long*)&stag[s], 0ull, (unsigned long long)tag);
                     if (t == 0) {
                         srec[s] = p | len << 40;
-                        sw[s][0] = make_uint4(w[0], w[1], w[2], w[3]);
-                        sw[s][1] = make_uint4(w[4], w[5], w[6], w[7]);
+                        *reinterpret_cast<uint4*>(&L.sw[s][0]) = make_uint4(w[0], w[1], w[2], w[3]);
+                        *reinterpret_cast<uint4*>(&L.sw[s][4]) = make_uint4(w[4], w[5], w[6], w[7]);
                         slot = (int)s;
                         break;
                     }
@@ -823,7 +833,8 @@ __global__ __launch_bounds__(LS_NT) void k_long_small(MapArgs a, u32 nreg) {
         bool fallback = valid && slot < 0;
         if (valid && slot >= 0) {
             const u64 rr = srec[slot];
-            if ((rr >> 40) == len && w8_same(w, sw[slot][0], sw[slot][1]) &&
+            if ((rr >> 40) == len && w8_same(w, *reinterpret_cast<const uint4*>(&L.sw[slot][0]),
+                                             *reinterpret_cast<const uint4*>(&L.sw[slot][4])) &&
                 long_rest_same(a, p, rr & LLOG_OFF_MASK, (u32)len))
                 atomicAdd((unsigned long long*)&scnt[slot], 1ull);
             else fallback = true;
@@ -838,7 +849,7 @@ __global__ __launch_bounds__(LS_NT) void k_long_small(MapArgs a, u32 nreg) {
         const u64 c = scnt[s];
         if (c == 0) continue;
         const u64 rr = srec[s], len = rr >> 40, p = rr & LLOG_OFF_MASK;
-        const uint4 x = sw[s][0], y = sw[s][1];
+        const uint4 x = *reinterpret_cast<const uint4*>(&L.sw[s][0]), y = *reinterpret_cast<const uint4*>(&L.sw[s][4]);
         const u32 w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
         ltab_add(a, len, stag[s], long_words(a, p, len, w), c, false);
     }

@@ -21,7 +21,7 @@ import check_inflight
 name = sys.argv[1]
 text = open(f"/tmp/var_{name}.s").read()
 e = []
-for sym in ("_ZN3wcg5k_mapILi0ELb1EEEvNS_7MapArgsE", "_ZN3wcg5k_mapILi0ELb0EEEvNS_7MapArgsE", "_ZN3wcg5k_aggILi0EEEvNS_7AggArgsE", "_ZN3wcg5k_aggILi1EEEvNS_7AggArgsE"):
+for sym in ("_ZN3wcg5k_mapILi0ELb1EEEvNS_7MapArgsE", "_ZN3wcg5k_mapILi0ELb0EEEvNS_7MapArgsE", "_ZN3wcg5k_aggILi0EEEvNS_7AggArgsENS_7MapArgsE", "_ZN3wcg5k_aggILi1EEEvNS_7AggArgsENS_7MapArgsE"):
     e += check_inflight.check(text, sym)[0]
 if e:
     os.remove(f"/root/repo/build/var/libwcg_{name}.so")
