@@ -45,6 +45,12 @@ constexpr int AGG_PROBES = WCG_AGG_PROBES;
 #define WCG_AGG_SPEC_K1 0      // 1: medium keys read their k1 rows with the k0 rows (measured slower on C2 and C4)
 #endif
 constexpr bool AGG_SPEC_K1 = WCG_AGG_SPEC_K1;
+#ifndef WCG_AGG_SPEC_MED
+#define WCG_AGG_SPEC_MED 1     // medium-only buckets (r06): k1 rows read with the k0 rows
+#endif
+#ifndef WCG_AGG_KINDS
+#define WCG_AGG_KINDS 1        // 0: split buckets aggregated by the any-key code (measurement)
+#endif
 #ifndef WCG_AGG_ABLATE
 #define WCG_AGG_ABLATE 0       // diagnostics: 1 = loads only, 2 = + decode and hash, 3 = no flush, 4 = short keys only (wrong counts)
 #endif
@@ -112,6 +118,34 @@ __device__ __forceinline__ void agg_decode(const u64 (&u)[6], u64 (&k0)[4], u64 
     }
 }
 
+// the same for buckets of one kind (r06, one-pass jobs: k_map logs short and medium keys to
+// separate buckets).  Short buckets hold short keys (T = length 1..7, U_CNT perhaps set) and count
+// units (T = 0); medium buckets hold heads (T >= 0x41), tails and count units (both skipped).
+__device__ __forceinline__ void agg_decode_short(const u64 (&u)[6], u64 (&k0)[4], u64 (&k1)[4], u64 (&c)[4], bool (&v)[4],
+                                                 u32 (&nu)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        v[k] = (u[k] >> 56) != 0;
+        const bool hc = (u[k] & U_CNT) != 0;
+        k0[k] = u[k] & ~U_CNT;
+        k1[k] = 0;
+        c[k] = hc ? u[k + 1] : 1;
+        nu[k] = hc ? 2u : 1u;
+    }
+}
+__device__ __forceinline__ void agg_decode_medium(const u64 (&u)[6], u64 (&k0)[4], u64 (&k1)[4], u64 (&c)[4], bool (&v)[4],
+                                                  u32 (&nu)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        v[k] = (u32)(u[k] >> 56) >= 0x41;
+        const bool hc = (u[k + 1] & U_CNT) != 0;
+        k0[k] = u[k];
+        k1[k] = u[k + 1] & ~U_CNT;
+        c[k] = hc ? u[k + 2] : 1;
+        nu[k] = hc ? 3u : 2u;
+    }
+}
+
 // k_agg's prefetch register sets: three tagged 16-byte loads per set and a wait naming the set's
 // registers (tools/check_inflight.py; the k_map sets use the same tags with one load each)
 #define WCG_AGG_SET_OPS(S)                                                                      \
@@ -143,7 +177,8 @@ WCG_AGG_SET_OPS(C)
 // One (bucket, slice) of k_agg: index bi = p + P * s.  Returns the global-table inserts made.
 // MODE is a template parameter: one kernel for both passes held the union of their registers
 // (128 VGPRs with a spill)
-template <int MODE>
+// KIND (r06): 0 = any keys; 1 / 2 = a short / medium bucket of a split one-pass log
+template <int MODE, int KIND>
 __device__ __forceinline__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_W], u64 (*tk1)[AGG_W], u64 (*tcnt)[AGG_W], u32* rlen_s,
                        u32* bstart, u32& spos, u64 (*wsum)[4]) {
     const int tid = threadIdx.x;
@@ -157,6 +192,9 @@ __device__ __forceinline__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_
     u32 p, s, sl;
     if (bi < a.pm * a.slices) { p = bi % a.pm; s = bi / a.pm; sl = a.slices; }
     else { const u32 b2 = bi - a.pm * a.slices, nm = a.P - a.pm; p = a.pm + b2 % nm; s = b2 / nm; sl = a.slices_m; }
+#ifdef WCG_AGG_MREV
+    if (p >= a.pm && a.pm < a.P) p = a.P - 1 - (p - a.pm);    // measurement: medium buckets reversed
+#endif
     u32 k0_, k1_, wbase, wstep;
     if (!emit) {
         k0_ = (u32)(((u64)a.nsrc * s) / sl); k1_ = (u32)(((u64)a.nsrc * (s + 1)) / sl);
@@ -260,7 +298,9 @@ __device__ __forceinline__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_
         u64 k0[4], k1[4], c[4];
         bool v[4];
         u32 nu[4];
-        agg_decode(u, k0, k1, c, v, nu);
+        if (KIND == 1) agg_decode_short(u, k0, k1, c, v, nu);
+        else if (KIND == 2) agg_decode_medium(u, k0, k1, c, v, nu);
+        else agg_decode(u, k0, k1, c, v, nu);
         if (WCG_AGG_ABLATE == 4) {            // diagnostics: short keys only (medium entries dropped)
 #pragma unroll
             for (int j = 0; j < 4; j++) v[j] = v[j] && key_short(k0[j]);
@@ -276,6 +316,9 @@ __device__ __forceinline__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_
         // lookup that inserts a key another of the lane's lookups also inserts may leave the key
         // in two slots: harmless, as between lanes)
         static_assert(4 % AGG_PROBES == 0, "probe groups split a lane's 4 units");
+        // a medium bucket reads its k1 rows with the k0 rows (every key needs them: no dependent
+        // read); mixed buckets do not (measured slower there: short keys paid the extra reads)
+        constexpr bool SPEC = KIND == 2 ? WCG_AGG_SPEC_MED : AGG_SPEC_K1;
 #pragma unroll
         for (int j = 0; j < 4; j += AGG_PROBES) {
             typename decltype(tab)::Probe pr[AGG_PROBES];
@@ -283,14 +326,14 @@ __device__ __forceinline__ u64 agg_one(const AggArgs& a, u32 bi, u64 (*tk0)[AGG_
             for (int q = 0; q < AGG_PROBES; q++) {
                 const u32 h = emit ? agg_hash(k0[j + q], k1[j + q]) : lds_hash(k0[j + q], k1[j + q]);
                 if (!v[j + q]) continue;
-                if (AGG_SPEC_K1) tab.start_k1(h, !key_short(k0[j + q]), pr[q]);
+                if (SPEC) tab.start_k1(h, KIND == 2 || !key_short(k0[j + q]), pr[q]);
                 else tab.start(h, pr[q]);
             }
 #pragma unroll
             for (int q = 0; q < AGG_PROBES; q++) {
                 if (!v[j + q]) continue;
-                const bool ok = AGG_SPEC_K1 ? tab.finish_k1(k0[j + q], k1[j + q], pr[q], c[j + q])
-                                            : tab.finish(k0[j + q], k1[j + q], pr[q], c[j + q]);
+                const bool ok = SPEC ? tab.template finish_k1<KIND>(k0[j + q], k1[j + q], pr[q], c[j + q])
+                                     : tab.template finish<KIND>(k0[j + q], k1[j + q], pr[q], c[j + q]);
                 if (!ok) overflow(k0[j + q], k1[j + q], c[j + q], nu[j + q]);
             }
         }
@@ -473,7 +516,11 @@ __global__ __launch_bounds__(AGG_NT) void k_agg(AggArgs a, MapArgs ma) {
     if (MODE == AGG_SPILL && blockIdx.x == 0 && tid == 0) { a.st->nrec = 0; a.st->nlong = 0; }
     u64 my_global = 0;
     for (u32 bi = blockIdx.x; bi < nb; bi += gridDim.x)
-        my_global += agg_one<MODE>(a, bi, tk0, tk1, tcnt, rlen_s, bstart, spos, wsum);
+        if (MODE == AGG_SPILL && WCG_AGG_KINDS && a.pm < a.P)    // split buckets: one kind each
+            my_global += bi < a.pm * a.slices ? agg_one<MODE, 1>(a, bi, tk0, tk1, tcnt, rlen_s, bstart, spos, wsum)
+                                              : agg_one<MODE, 2>(a, bi, tk0, tk1, tcnt, rlen_s, bstart, spos, wsum);
+        else
+            my_global += agg_one<MODE, 0>(a, bi, tk0, tk1, tcnt, rlen_s, bstart, spos, wsum);
     // one atomic per workgroup (a per-wave atomic on one DevState line serialises)
     for (int d = 32; d >= 1; d >>= 1) my_global += __shfl_xor(my_global, d, 64);
     u64 ms = 0;

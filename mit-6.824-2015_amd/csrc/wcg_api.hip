@@ -1278,6 +1278,17 @@ int agg_clock_report(wcg_ctx* c, const AggArgs& g, u32 nb1, u64 grid) {
         const int kind = bi >= g.pm * g.slices;
         kd[kind] += d; km[kind] = std::max(km[kind], d); ku[kind] += (double)units[bi]; kn[kind]++;
     }
+    {   // the five slowest workgroups
+        std::vector<u32> ord(nb1);
+        for (u32 i = 0; i < nb1; i++) ord[i] = i;
+        std::sort(ord.begin(), ord.end(), [&](u32 x, u32 y) { return clk[2 * x + 1] - clk[2 * x] > clk[2 * y + 1] - clk[2 * y]; });
+        for (u32 r = 0; r < std::min<u32>(5, nb1); r++) {
+            const u32 bi = ord[r];
+            fprintf(stderr, "wcg k_agg clock: slow #%u bi %u (%s) dur %.1f us units %llu\n", r, bi,
+                    bi >= g.pm * g.slices ? "medium" : "short", (clk[2 * bi + 1] - clk[2 * bi]) / 100.0,
+                    (unsigned long long)units[bi]);
+        }
+    }
     for (int kind = 0; kind < 2; kind++)
         if (kn[kind])
             fprintf(stderr, "wcg k_agg clock: %s workgroups %u, dur mean %.1f max %.1f us, units mean %.0f\n",

@@ -99,6 +99,7 @@ struct LdsTable {
 
     // finish() after start_k1: a match is decided from the rows already read (short keys have
     // k1 == 0 and compare with the zeros start_k1 put there); the insert path is finish()'s
+    template <int KIND = 0>
     __device__ __forceinline__ bool finish_k1(u64 a0, u64 a1, const Probe& p, CNT c) {
         u32 m = 0;
 #pragma unroll
@@ -111,14 +112,16 @@ struct LdsTable {
             add_cnt(s < W ? p.b1 : p.b2, s % W, c);
             return true;
         }
-        return finish(a0, a1, p, c);
+        return finish<KIND>(a0, a1, p, c);
     }
 
     // match (slot s: bucket b1 for s < W, else b2; way s % W) or insert; false when both
     // buckets are full of other keys.  Straight-line common path: bit masks and one atomic at a
-    // computed address.
+    // computed address.  KIND: 0 = any key, 1 = short keys only, 2 = medium keys only (k_agg's
+    // split buckets, r06: the key-length tests fold away)
+    template <int KIND = 0>
     __device__ __forceinline__ bool finish(u64 a0, u64 a1, const Probe& p, CNT c) {
-        const bool shrt = key_short(a0);
+        const bool shrt = KIND == 1 ? true : KIND == 2 ? false : key_short(a0);
         u32 m = 0, e = 0;
 #pragma unroll
         for (int j = 0; j < W; j++) {
