@@ -1278,6 +1278,16 @@ int agg_clock_report(wcg_ctx* c, const AggArgs& g, u32 nb1, u64 grid) {
         const int kind = bi >= g.pm * g.slices;
         kd[kind] += d; km[kind] = std::max(km[kind], d); ku[kind] += (double)units[bi]; kn[kind]++;
     }
+    static const char* dump = getenv("WCG_AGG_CLOCK_DUMP");   // path: every workgroup's line
+    if (dump) {
+        if (FILE* f = fopen(dump, "a")) {
+            for (u32 bi = 0; bi < nb1; bi++)
+                fprintf(f, "%u %u %llu %.2f %.2f\n", bi, (u32)(bi >= g.pm * g.slices), (unsigned long long)units[bi],
+                        (clk[2 * bi] - t0) / 100.0, (clk[2 * bi + 1] - clk[2 * bi]) / 100.0);
+            fprintf(f, "--\n");
+            fclose(f);
+        }
+    }
     {   // the five slowest workgroups
         std::vector<u32> ord(nb1);
         for (u32 i = 0; i < nb1; i++) ord[i] = i;

@@ -949,6 +949,10 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 x) {
 #ifndef WCG_UL_K
 #define WCG_UL_K 1
 #endif
+#ifndef WCG_UL_PIPE
+#define WCG_UL_PIPE 1                        // r06: pipelined rounds (UL_K = 1 only)
+#endif
+static_assert(!WCG_UL_PIPE || WCG_UL_K == 1, "the pipelined decode rounds take one lead per lane");
 constexpr int UL_K = WCG_UL_K;                // leads per lane per decode round (C4 k_map: 1 2.01-2.03 ms,
                                               // 2 2.11, 4 2.29-2.31: the rounds past the list's end
                                               // decode nothing at full VALU cost; 8 slots 2.04-2.06)
@@ -962,6 +966,9 @@ __device__ __forceinline__ u32 utf8_mask_list(uint4 c, u32 nx, LdsLetters lt, co
                      (cont_mask4(c.w) << 12) | (cont_mask4(nx) << 16);   // bit j: byte j
     u32 L = (lead_mask4(c.x) | (lead_mask4(c.y) << 4) | (lead_mask4(c.z) << 8) | (lead_mask4(c.w) << 12)) &
             (cont >> 1);                      // <= 8 per chunk (a lead's next byte is no lead)
+#ifdef WCG_UL_ABL
+    if (WCG_UL_ABL >= 2) L = 0;               // diagnostics (wrong masks): no lead list
+#endif
     const u32 nl = (u32)__popc(L);
     const u32 incl = wave_incl_scan(nl);
     const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
@@ -973,6 +980,59 @@ __device__ __forceinline__ u32 utf8_mask_list(uint4 c, u32 nx, LdsLetters lt, co
     }
     wave_lds_sync();
     u32* const wm32 = reinterpret_cast<u32*>(wm);
+#ifdef WCG_UL_ABL
+    if (WCG_UL_ABL >= 1) return wm[lane] | (tot & 0x10000u);   // diagnostics (wrong masks): no decode
+#endif
+#if WCG_UL_PIPE
+    // r06: the rounds software-pipelined (one lead per lane per round): round r + 1's list entry
+    // and bytes are read while round r is decoded and looked up, so a round's dependent chain is
+    // two LDS round trips (block id, letter bits) instead of four (+ the list entry and the
+    // bytes).  C4: the rounds were 0.70 ms of k_map's 1.94 (r06_experiments, WCG_UL_ABL)
+    if (tot) {
+        auto entry = [&](u32 base) -> u32 { return list[(base + lane) & (MAP_SST - 1)]; };
+        auto pos = [&](u32 base, u32 e) -> u32 { return base + lane < tot ? e & (MAP_WIN - 1) : 0u; };
+        auto word = [&](u32 q0) -> u32 {
+            const u32* q = reinterpret_cast<const u32*>(bytes + (q0 & ~3u));
+            return __builtin_amdgcn_alignbyte(q[1], q[0], q0 & 3u);
+        };
+        u32 p = pos(0, entry(0));
+        u32 wd = word(p);
+        for (u32 base = 0; base < tot; base += 64) {
+            const u32 en = entry(base + 64);              // the next round's entry (unused past tot)
+            __builtin_amdgcn_sched_barrier(0);
+            const bool act = base + lane < tot;
+            const u32 room = (u32)MAP_WIN - p;            // bytes past the window read as 0
+            const u32 x0 = wd & (room >= 4 ? 0xFFFFFFFFu : (1u << (8 * room)) - 1u);
+            const u32 b0 = x0 & 0xFFu;                    // C2-F4 (a listed lead)
+            const u32 w = __builtin_clz(~(x0 << 24));     // 2-4
+            const u32 need = (0xFFFFFFFFu >> ((32 - 8 * w) & 31)) & 0xFFFFFF00u;   // bytes 1..w-1
+            const bool conts = (((x0 & 0xC0C0C0C0u) ^ 0x80808080u) & need) == 0u;
+            const u32 x = ((b0 & (0x7Fu >> (w & 31))) << 18) | ((x0 << 4) & 0x3F000u) | ((x0 >> 10) & 0xFC0u) |
+                          ((x0 >> 24) & 0x3Fu);
+            const u32 v = x >> ((24 - 6 * w) & 31);
+            const bool ok = act & conts & ((v >> ((5 * w - 4) & 31)) != 0u) & (v - 0xD800u >= 0x800u) &
+                            (v <= 0x10FFFFu);
+            const u32 cp = ok ? v : 0u;
+            const u32 b = cp >> 8;
+            const u32 t = lt.idx[b < LT_LDS_BLOCKS ? b : LT_LDS_BLOCKS];
+            __builtin_amdgcn_sched_barrier(0);
+            const u32 pn = pos(base + 64, en);             // the next round's bytes, read behind the
+            const u32 wdn = word(pn);                      // block id
+            __builtin_amdgcn_sched_barrier(0);
+            const u32 bits = lt.bits[(b < 8 ? b : t) * 8 + ((cp >> 5) & 7)];
+            __builtin_amdgcn_sched_barrier(0);
+            if ((bits >> (cp & 31)) & 1u) {
+                const u32 own = p >> 4;
+                const u32 span = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0, w & 31) << (p & 15u);
+                atomicOr(&wm32[own >> 1], (span & 0xFFFFu) << (16 * (own & 1)));
+                if ((span >> 16) && own < 63)                  // into the next chunk's word
+                    atomicOr(&wm32[(own + 1) >> 1], (span >> 16) << (16 * ((own + 1) & 1)));
+            }
+            p = pn;
+            wd = wdn;
+        }
+    }
+#else
     // UL_K leads per lane per round, each stage's LDS reads issued together (one round trip per
     // stage, not per lead: the list entry, the bytes, the block id, the letter bits)
     for (u32 base = 0; base < tot; base += 64 * UL_K) {
@@ -1026,6 +1086,7 @@ __device__ __forceinline__ u32 utf8_mask_list(uint4 c, u32 nx, LdsLetters lt, co
                 atomicOr(&wm32[(own + 1) >> 1], (span >> 16) << (16 * ((own + 1) & 1)));
         }
     }
+#endif
     wave_lds_sync();
     return wm[lane];
 }
