@@ -949,6 +949,9 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 x) {
 #ifndef WCG_UL_K
 #define WCG_UL_K 1
 #endif
+#ifndef WCG_UL_MASKED
+#define WCG_UL_MASKED 0                      // pipelined rounds: exec-masked block-id / bits reads
+#endif
 #ifndef WCG_UL_PIPE
 #define WCG_UL_PIPE 1                        // r06: pipelined rounds (UL_K = 1 only)
 #endif
@@ -1014,12 +1017,24 @@ __device__ __forceinline__ u32 utf8_mask_list(uint4 c, u32 nx, LdsLetters lt, co
                             (v <= 0x10FFFFu);
             const u32 cp = ok ? v : 0u;
             const u32 b = cp >> 8;
+#if WCG_UL_MASKED
+            // only the lanes that need them read the block id (3- and 4-byte runes) and the bits
+            // (a letter candidate): fewer lanes in the random-address LDS reads
+            u32 t = 0;
+            if (b >= 8) t = lt.idx[b < LT_LDS_BLOCKS ? b : LT_LDS_BLOCKS];
+#else
             const u32 t = lt.idx[b < LT_LDS_BLOCKS ? b : LT_LDS_BLOCKS];
+#endif
             __builtin_amdgcn_sched_barrier(0);
             const u32 pn = pos(base + 64, en);             // the next round's bytes, read behind the
             const u32 wdn = word(pn);                      // block id
             __builtin_amdgcn_sched_barrier(0);
+#if WCG_UL_MASKED
+            u32 bits = 0;
+            if (cp) bits = lt.bits[(b < 8 ? b : t) * 8 + ((cp >> 5) & 7)];
+#else
             const u32 bits = lt.bits[(b < 8 ? b : t) * 8 + ((cp >> 5) & 7)];
+#endif
             __builtin_amdgcn_sched_barrier(0);
             if ((bits >> (cp & 31)) & 1u) {
                 const u32 own = p >> 4;
