@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--sync-steps", action="store_true",
                     help="N = 1: every timed step waits for its reduce (wcg_reduce) instead of queuing the "
                          "next job behind it (wcg_reduce_async)")
+    ap.add_argument("--one-context", action="store_true",
+                    help="N = 1: skip the loop whose jobs alternate between two engines on two streams")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N > 1 path with host-staged records, ranks may share a GPU")
     # below the driver's 600 s bench limit, so that the launcher's own bounded stop (and every
@@ -291,6 +293,16 @@ def main():
     # one stream for the engine's kernels and the collectives (stream-ordered hand-overs, no host
     # waits between export, all-to-all and import)
     work = torch.cuda.Stream()
+    # N = 1: the second engine's stream, next to the first so that HIP gives the two different
+    # hardware queues (GPU_MAX_HW_QUEUES = 4 here; first used only in the two-context loop, it got
+    # `work`'s queue and the two engines' jobs ran one after the other: r06_experiments)
+    stream2 = torch.cuda.Stream() if world == 1 else None
+    # (the queue is dealt at a stream's first use: both streams are used here, one after the other)
+    for s_ in (work, stream2):
+        if s_ is not None:
+            with torch.cuda.stream(s_):
+                torch.zeros(1, device=f"cuda:{local}")
+    torch.cuda.synchronize()
     torch.cuda.set_stream(work)
     stream = work.cuda_stream
     # table capacity: twice the vocabulary, but no more keys than one per 32 input bytes (C4's densest
@@ -348,6 +360,33 @@ def main():
         nstep[0] += 1
 
     pipe = world == 1 and not args.sync_steps
+    # N = 1 (r06): jobs may also alternate between two engines (contexts) on two streams: each job
+    # is the same full reset + map + reduce, but the next job's k_map starts on the CUs that the
+    # previous job's aggregation tail and one-launch reduce leave idle (one engine's jobs are
+    # strictly ordered on its stream).  An engine's previous job is waited for (its status read
+    # back) before the engine is reused; both engines' last outputs are verified below.
+    two = pipe and not args.one_context
+    engs, pend = [eng], [False, False]
+    if two:
+        eng2 = wcg.Engine(device=local, max_input_bytes=0, max_keys=keys_cap)
+        eng2.set_stream(stream2.cuda_stream)
+        engs.append(eng2)
+
+    def step2(i):
+        j = i % 2
+        if pend[j]:
+            engs[j].reduce_wait()
+        engs[j].reset()
+        engs[j].map_device(dev.data_ptr(), n)
+        engs[j].reduce_async()
+        pend[j] = True
+
+    def drain2():
+        for j in range(len(engs)):
+            if pend[j]:
+                engs[j].reduce_wait()
+                pend[j] = False
+
     for _ in range(args.warmup):
         step(pipe)
     if pipe:
@@ -389,6 +428,20 @@ def main():
         torch.cuda.synchronize()
         synced_ms = (time.perf_counter() - ts) / args.steps * 1e3
         step_ms = [(b - a) * 1e3 for a, b in zip(marks, marks[1:])]
+    two_ms = None
+    if two:
+        # the third loop (after W warm-up jobs of its own): K jobs alternating between the engines
+        eng.enable_timing(0)
+        for i in range(args.warmup):
+            step2(i)
+        drain2()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        for i in range(args.steps):
+            step2(i)
+        drain2()                                  # every job's read-back (errors surface here)
+        torch.cuda.synchronize()
+        two_ms = (time.perf_counter() - t2) / args.steps * 1e3
     stats = eng.stats()
     # every phase (events around each), on instrumented steps after the timed region; N > 1 also
     # times the step's stages on the host clock with a synchronise after each (the shuffle through
@@ -436,7 +489,8 @@ def main():
         from tests import oracle_bridge as ob
         data = host.numpy().tobytes()
         if world == 1:
-            verified = eng.result() == ob.merged(data, 16)
+            want = ob.merged(data, 16)
+            verified = all(e.result() == want for e in engs)   # two contexts: both engines' last job
         else:
             # every rank counts its own range with the oracle; root sums the counts of all ranks
             # and compares the merged file the GPUs left in root's HBM
@@ -461,15 +515,18 @@ def main():
 
     if rank == 0:
         ms_step = dt / args.steps * 1e3
-        # N = 1: two K-step loops ran the same full jobs (pipelined: reset, map, wcg_reduce_async
-        # back to back; synced: every job waits for its reduce's read-back), each bracketed by
-        # torch.cuda.synchronize(); the faster one is the value and step_mode names it (on the
-        # round-5 driver box the synced loop was the faster by 0.9 %, on the builder's box the
-        # pipelined one by 1.7 %: box-to-box variance)
+        # N = 1: two or three K-step loops ran the same full jobs (two_contexts: jobs alternate
+        # between two engines on two streams; pipelined: reset, map, wcg_reduce_async back to back
+        # on one engine; synced: every job waits for its reduce's read-back), each bracketed by
+        # torch.cuda.synchronize(); the fastest is the value and step_mode names it (on the
+        # round-5 driver box the synced loop was the faster of the one-engine loops by 0.9 %, on
+        # the builder's box the pipelined one by 1.7 %: box-to-box variance)
         mode_used = "pipelined" if pipe else "synced"
         ms_pipelined = ms_step if pipe else None
         if synced_ms is not None and synced_ms < ms_step:
             ms_step, dt, mode_used = synced_ms, synced_ms * args.steps / 1e3, "synced"
+        if two_ms is not None and two_ms < ms_step:
+            ms_step, dt, mode_used = two_ms, two_ms * args.steps / 1e3, "two_contexts"
         all_bytes = total if strong else n * world
         gbs = all_bytes / (dt / args.steps) / 1e9
         avg_map_ms = map_sum["map"] / args.steps      # HIP events over the timed steps
@@ -522,12 +579,24 @@ def main():
         out["ms_per_step_spread"] = {"min": q(0.0), "p10": q(0.1), "p90": q(0.9), "max": q(1.0),
                                      "how": ("host clock between the steps of a second K-step loop in which "
                                              "every step waits for its reduce (wcg_reduce); value uses the "
-                                             "mean over the faster of the two bracketed loops (step_mode)" if pipe else
+                                             "mean over the fastest of the bracketed loops (step_mode)" if pipe else
                                              "host clock between steps (each step ends in a host wait); "
                                              "value uses the mean over the bracketed loop")}
-        out["step_mode"] = ("pipelined: reset, map, wcg_reduce_async per job, back to back on one stream; "
-                            "the last job's read-back waited for inside the timed region" if mode_used == "pipelined" else
-                            "synchronous: each job ends in its reduce's host read-back (wcg_reduce)")
+        out["step_mode"] = {
+            "two_contexts": "two contexts: jobs alternate between two engines on two streams (reset, map, "
+                            "wcg_reduce_async; an engine's previous job is waited for before its reuse), so one "
+                            "job's map runs on the CUs the other's aggregation tail and reduce leave idle; every "
+                            "job runs in full, both engines' last outputs verified; the last jobs' read-backs "
+                            "waited for inside the timed region",
+            "pipelined": "pipelined: reset, map, wcg_reduce_async per job, back to back on one stream; the last "
+                         "job's read-back waited for inside the timed region",
+            "synced": "synchronous: each job ends in its reduce's host read-back (wcg_reduce)"}[mode_used]
+        if two_ms is not None:
+            out["loop_order"] = ("after W warm-up jobs: the pipelined loop (the first, so it carries the GPU's "
+                                 "clock ramp from idle), the synced loop, then W more warm-up jobs and the "
+                                 "two-context loop")
+            out["ms_per_step_two_contexts"] = round(two_ms, 4)
+            out["value_two_contexts"] = round(all_bytes / (two_ms * 1e-3) / 1e9, 3)
         if synced_ms is not None:
             out["ms_per_step_pipelined"] = round(ms_pipelined, 4)
             out["value_pipelined"] = round(all_bytes / (ms_pipelined * 1e-3) / 1e9, 3)

@@ -1375,6 +1375,9 @@ int wcg_map_device(wcg_ctx* c, const void* dev_bytes, uint64_t n) {
     // offsets fit 32 bits and its 24-bit multiplies (P * region_cap * 8 <= 2^31)
     // (split buckets: every region sized like an unsplit bucket's)
     a.region_cap = std::min<u64>(std::max<u64>(2048, per_wg_bytes / (4ull * MISS_SHORT_BUCKETS)), (1ull << 31) / (8ull * P)) & ~1ull;
+    static const char* rpad_env = getenv("WCG_REGION_PAD");   // measurement: units added to a region
+    if (rpad_env && a.region_cap + (u64)(atoi(rpad_env) & ~1) <= (1ull << 31) / (8ull * P))
+        a.region_cap += (u64)(atoi(rpad_env) & ~1);
     a.pmask = P - 1;
     u64 need = (grid * P * a.region_cap + AGG_SLACK_UNITS) * sizeof(u64);
     if (need > c->pool_bytes) {
