@@ -51,8 +51,9 @@ def parse():
     ap.add_argument("--sync-steps", action="store_true",
                     help="N = 1: every timed step waits for its reduce (wcg_reduce) instead of queuing the "
                          "next job behind it (wcg_reduce_async)")
-    ap.add_argument("--one-context", action="store_true",
-                    help="N = 1: skip the loop whose jobs alternate between two engines on two streams")
+    ap.add_argument("--contexts", type=int, default=2,
+                    help="N = 1: engines (each on its own stream) the multi-context loop deals its jobs to; "
+                         "1 skips that loop (at most 4: one hardware queue each)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N > 1 path with host-staged records, ranks may share a GPU")
     # below the driver's 600 s bench limit, so that the launcher's own bounded stop (and every
@@ -293,15 +294,15 @@ def main():
     # one stream for the engine's kernels and the collectives (stream-ordered hand-overs, no host
     # waits between export, all-to-all and import)
     work = torch.cuda.Stream()
-    # N = 1: the second engine's stream, next to the first so that HIP gives the two different
-    # hardware queues (GPU_MAX_HW_QUEUES = 4 here; first used only in the two-context loop, it got
-    # `work`'s queue and the two engines' jobs ran one after the other: r06_experiments)
-    stream2 = torch.cuda.Stream() if world == 1 else None
-    # (the queue is dealt at a stream's first use: both streams are used here, one after the other)
-    for s_ in (work, stream2):
-        if s_ is not None:
-            with torch.cuda.stream(s_):
-                torch.zeros(1, device=f"cuda:{local}")
+    # N = 1: the other engines' streams, next to the first so that HIP gives each its own hardware
+    # queue (GPU_MAX_HW_QUEUES = 4 here; a second stream first used only in the multi-context loop
+    # got `work`'s queue and the two engines' jobs ran one after the other: r06_experiments)
+    nctx = max(1, min(args.contexts, 4)) if world == 1 else 1
+    xstreams = [torch.cuda.Stream() for _ in range(nctx - 1)]
+    # (the queue is dealt at a stream's first use: the streams are used here, one after another)
+    for s_ in [work] + xstreams:
+        with torch.cuda.stream(s_):
+            torch.zeros(1, device=f"cuda:{local}")
     torch.cuda.synchronize()
     torch.cuda.set_stream(work)
     stream = work.cuda_stream
@@ -360,20 +361,21 @@ def main():
         nstep[0] += 1
 
     pipe = world == 1 and not args.sync_steps
-    # N = 1 (r06): jobs may also alternate between two engines (contexts) on two streams: each job
-    # is the same full reset + map + reduce, but the next job's k_map starts on the CUs that the
-    # previous job's aggregation tail and one-launch reduce leave idle (one engine's jobs are
-    # strictly ordered on its stream).  An engine's previous job is waited for (its status read
-    # back) before the engine is reused; both engines' last outputs are verified below.
-    two = pipe and not args.one_context
-    engs, pend = [eng], [False, False]
+    # N = 1 (r06): jobs may also be dealt in turn to several engines (contexts), each on its own
+    # stream: every job is the same full reset + map + reduce, but the next job's k_map starts on
+    # the CUs that the previous job's aggregation tail and one-launch reduce leave idle (one
+    # engine's jobs are strictly ordered on its stream).  An engine's previous job is waited for
+    # (its status read back) before the engine is reused; every engine's last output is verified.
+    two = pipe and nctx > 1
+    engs, pend = [eng], [False] * nctx
     if two:
-        eng2 = wcg.Engine(device=local, max_input_bytes=0, max_keys=keys_cap)
-        eng2.set_stream(stream2.cuda_stream)
-        engs.append(eng2)
+        for s_ in xstreams:
+            e_ = wcg.Engine(device=local, max_input_bytes=0, max_keys=keys_cap)
+            e_.set_stream(s_.cuda_stream)
+            engs.append(e_)
 
     def step2(i):
-        j = i % 2
+        j = i % len(engs)
         if pend[j]:
             engs[j].reduce_wait()
         engs[j].reset()
@@ -490,7 +492,7 @@ def main():
         data = host.numpy().tobytes()
         if world == 1:
             want = ob.merged(data, 16)
-            verified = all(e.result() == want for e in engs)   # two contexts: both engines' last job
+            verified = all(e.result() == want for e in engs)   # several contexts: every engine's last job
         else:
             # every rank counts its own range with the oracle; root sums the counts of all ranks
             # and compares the merged file the GPUs left in root's HBM
@@ -515,8 +517,8 @@ def main():
 
     if rank == 0:
         ms_step = dt / args.steps * 1e3
-        # N = 1: two or three K-step loops ran the same full jobs (two_contexts: jobs alternate
-        # between two engines on two streams; pipelined: reset, map, wcg_reduce_async back to back
+        # N = 1: two or three K-step loops ran the same full jobs (contexts: jobs dealt in turn to
+        # --contexts engines on their own streams; pipelined: reset, map, wcg_reduce_async back to back
         # on one engine; synced: every job waits for its reduce's read-back), each bracketed by
         # torch.cuda.synchronize(); the fastest is the value and step_mode names it (on the
         # round-5 driver box the synced loop was the faster of the one-engine loops by 0.9 %, on
@@ -526,7 +528,7 @@ def main():
         if synced_ms is not None and synced_ms < ms_step:
             ms_step, dt, mode_used = synced_ms, synced_ms * args.steps / 1e3, "synced"
         if two_ms is not None and two_ms < ms_step:
-            ms_step, dt, mode_used = two_ms, two_ms * args.steps / 1e3, "two_contexts"
+            ms_step, dt, mode_used = two_ms, two_ms * args.steps / 1e3, "contexts"
         all_bytes = total if strong else n * world
         gbs = all_bytes / (dt / args.steps) / 1e9
         avg_map_ms = map_sum["map"] / args.steps      # HIP events over the timed steps
@@ -583,20 +585,21 @@ def main():
                                              "host clock between steps (each step ends in a host wait); "
                                              "value uses the mean over the bracketed loop")}
         out["step_mode"] = {
-            "two_contexts": "two contexts: jobs alternate between two engines on two streams (reset, map, "
-                            "wcg_reduce_async; an engine's previous job is waited for before its reuse), so one "
-                            "job's map runs on the CUs the other's aggregation tail and reduce leave idle; every "
-                            "job runs in full, both engines' last outputs verified; the last jobs' read-backs "
-                            "waited for inside the timed region",
+            "contexts": f"{nctx} contexts: jobs dealt in turn to {nctx} engines, each on its own stream and "
+                        "hardware queue (reset, map, wcg_reduce_async; an engine's previous job is waited for "
+                        "before its reuse), so one job's map runs on the CUs another's aggregation tail and "
+                        "reduce leave idle; every job runs in full, every engine's last output verified; the "
+                        "last jobs' read-backs waited for inside the timed region",
             "pipelined": "pipelined: reset, map, wcg_reduce_async per job, back to back on one stream; the last "
                          "job's read-back waited for inside the timed region",
             "synced": "synchronous: each job ends in its reduce's host read-back (wcg_reduce)"}[mode_used]
         if two_ms is not None:
             out["loop_order"] = ("after W warm-up jobs: the pipelined loop (the first, so it carries the GPU's "
                                  "clock ramp from idle), the synced loop, then W more warm-up jobs and the "
-                                 "two-context loop")
-            out["ms_per_step_two_contexts"] = round(two_ms, 4)
-            out["value_two_contexts"] = round(all_bytes / (two_ms * 1e-3) / 1e9, 3)
+                                 "multi-context loop")
+            out["contexts"] = nctx
+            out["ms_per_step_contexts"] = round(two_ms, 4)
+            out["value_contexts"] = round(all_bytes / (two_ms * 1e-3) / 1e9, 3)
         if synced_ms is not None:
             out["ms_per_step_pipelined"] = round(ms_pipelined, 4)
             out["value_pipelined"] = round(all_bytes / (ms_pipelined * 1e-3) / 1e9, 3)

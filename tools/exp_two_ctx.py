@@ -2,7 +2,7 @@
 """Measurement (r06): C2 jobs on ONE engine back to back (the bench's pipelined loop) against jobs
 alternating between TWO engines on two streams, so that one job's map can start on the CUs the
 other job's aggregation tail and reduce leave idle.  Every job runs in full; the last job of each
-engine is checked against the oracle.  Usage: tools/exp_two_ctx.py [steps] [streams-first|bench]"""
+engine is checked against the oracle.  Usage: tools/exp_two_ctx.py [steps] [streams-first|bench] [contexts]"""
 import os
 import sys
 import time
@@ -23,9 +23,10 @@ dev = host.to("cuda:0")
 torch.cuda.synchronize()
 keys_cap = max(min(2 * cfg["vocab"], n // 32), 1 << 18)
 order = sys.argv[2] if len(sys.argv) > 2 else "streams-first"
+nctx = int(sys.argv[3]) if len(sys.argv) > 3 else 2
 engs = []
-if order == "streams-first":          # both streams, then both engines
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+if order == "streams-first":          # the streams, then the engines
+    streams = [torch.cuda.Stream() for _ in range(nctx)]
     for s in streams:
         e = wcg.Engine(device=0, max_input_bytes=0, max_keys=keys_cap)
         e.set_stream(s.cuda_stream)
@@ -68,7 +69,7 @@ def run(neng, k):
 
 
 for rep in range(2):
-    for neng in (1, 2):
+    for neng in range(1, nctx + 1):
         run(neng, 10)                               # warm-up
         ms = run(neng, steps)
         print(f"engines {neng}: {ms:.4f} ms/job = {n / ms / 1e6:.1f} GB/s", flush=True)
