@@ -567,7 +567,11 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic, "avg_launch_ms": round(avg_map_ms, 4),
-                         "algorithmic_bytes_per_launch": n},
+                         "algorithmic_bytes_per_launch": n,
+                         "measured_on": "HIP events around every k_map launch of the one-engine pipelined loop "
+                                        "(each launch alone on the GPU; in the multi-context loop two jobs' "
+                                        "kernels share the CUs)" if pipe else
+                                        "HIP events around every k_map launch of the timed loop"},
         }
         # per-step spread (host clock between steps; N > 1: each step's slowest rank)
         if world > 1:
