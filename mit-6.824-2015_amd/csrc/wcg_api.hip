@@ -1234,7 +1234,9 @@ int reset_tables(wcg_ctx* c) {
     // one launch clears the tables and the counters (three memsets were three dispatches)
     if (!clear_g) g16 = 0;
     static_assert(sizeof(GEntry) == 32, "k_clear's listed entries are two 16-byte words");
-    k_clear<<<grid_for(g16 + l16, 256, c->ncu * 4), 256, 0, c->stream>>>(
+    static const char* cg_env = getenv("WCG_CLEAR_GRID");       // measurement: workgroups of k_clear
+    const u64 cgrid = cg_env ? std::max<u64>(1, (u64)atoi(cg_env)) : grid_for(g16 + l16, 256, c->ncu * 4);
+    k_clear<<<(unsigned)cgrid, 256, 0, c->stream>>>(
         reinterpret_cast<uint4*>(c->gtab), g16, reinterpret_cast<uint4*>(c->ltab), l16, c->st, glist, llist);
     HIPCHK(c, hipGetLastError());
     c->gtab_zero = true;
