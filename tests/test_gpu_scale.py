@@ -5,7 +5,8 @@
   * C4's key cardinality: the first GiB of the C4 generator (2.4e7 distinct keys) through
     several wcg_map_device calls into one context sized for 5e7 keys;
   * the 64 GiB job's call size: 16 GiB of C4 in two 8 GiB calls, verified exactly;
-  * a C3-shaped job: 2 GiB of the C3 generator, nReduce = 64, all 64 -res-<r> files.
+  * a C3-shaped job: 2 GiB of the C3 generator, nReduce = 64, all 64 -res-<r> files;
+  * C3 at its full size: 16 GiB in one wcg_map_device call, verified exactly (r06).
 """
 import pytest
 
@@ -178,3 +179,47 @@ def test_c3_shaped_2gib_nreduce_64(built):
     r = ob.Result(host.numpy().tobytes(), 16)
     ob.assert_same(merged, r.merged())
     assert parts == [r.res(64, i) for i in range(64)]
+
+
+@pytest.mark.timeout(600)
+def test_c3_full_16gib_one_call(built):
+    """BASELINE config 3 at its full size on one GPU, as bench.py maps it: 16 GiB of the C3 generator
+    in ONE wcg_map_device call (the miss log, region sizes and 32-bit unit offsets at their largest
+    one-pass extent), then DoReduce + Merge; checked exactly by the oracle's verifier (every input
+    token decrements its line's count; keys strictly ascending).  ~1-2 minutes."""
+    import threading
+    import time
+    import numpy as np
+    import torch
+    import wcg
+    from wcg.corpus import Generator, CONFIGS, BLOCK
+    cfg = CONFIGS["c3_ascii_zipf_16gib"]
+    gen = Generator(cfg["mode"], cfg["vocab"], cfg["zipf_s"], cfg["seed"])
+    n, gib = 16 << 30, 1 << 30
+    host = np.empty(n, dtype=np.uint8)
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for g in range(n // gib):
+        a = g * gib
+        gen.fill_ptr(host.ctypes.data + a, gib, first_block=a // BLOCK, threads=16)
+        dev[a:a + gib].copy_(torch.from_numpy(host[a:a + gib]))
+    torch.cuda.synchronize()
+    print("c3 16 GiB: generated", flush=True)
+    keys_cap = max(min(2 * cfg["vocab"], n // 32), 1 << 18)     # as bench.py sizes it
+    with wcg.Engine(0, 0, keys_cap) as e:
+        e.reset()
+        e.map_device(dev.data_ptr(), n)
+        nk, _ = e.reduce()
+        got = e.result()
+        st = e.stats()
+    del dev
+    assert st["overflow"] == 0 and nk == cfg["vocab"]
+    res = {}
+    th = threading.Thread(target=lambda: res.update(v=ob.verify_merged(host.ctypes.data, n, got, 16)), daemon=True)
+    t0 = time.perf_counter()
+    th.start()
+    while th.is_alive():
+        th.join(20)
+        print(f"c3 16 GiB: verifying ({time.perf_counter() - t0:.0f} s)", flush=True)
+    ok, msg, ntok, nkeys = res["v"]
+    assert ok, msg
+    assert ntok == st["tokens"] and nkeys == nk
